@@ -1,0 +1,181 @@
+/*
+ * wbc.h — C-ABI of the MI355X batched whole-body-control engine.
+ *
+ * Drop-in boundary for the per-cycle hot path of the reference's `WholeBodyController`
+ * (include/anymal_wbc/whole_body_controller.hpp:35-171, src/whole_body_controller.cpp:256-577):
+ *
+ *   reference call (file:line)                                   -> C-ABI entry point
+ *   WholeBodyController::WholeBodyController()  cpp:22-59         -> wbc_create
+ *   WholeBodyController::~WholeBodyController() cpp:61-63         -> wbc_destroy
+ *   loadParameters()                            cpp:122-148       -> wbc_params (wbc_default_params)
+ *   ModelLoader::loadModelFromFile(urdf)        cpp:26-40         -> wbc_model (wbc_anymal_model)
+ *   floatingBaseStateCallback/jointStateCallback cpp:187-254      -> wbc_set_state
+ *   referenceCallback(WbcReferenceMsg)          cpp:150-185       -> wbc_set_reference
+ *   setInitialState() + firstControllerIteration_ cpp:65-120,523  -> wbc_reset
+ *   updateState()                               cpp:256-294       -> wbc_update
+ *   solveQP() + computeJointTorques()           cpp:466-577       -> wbc_solve
+ *   controlLoop() body (update; solve; torques) cpp:650-652       -> wbc_step (fused)
+ *   jointTorquePub_/desiredGroundReactionForcesPub_ cpp:563,576   -> wbc_get_output
+ *   qpReturnValue_ != SUCCESSFUL_RETURN          cpp:654           -> per-robot status[] (WBC_QP_*)
+ *
+ * Conventions
+ *  - Everything is fp64.  Sizes are compile-time constants of the reference (hpp:27-32).
+ *  - A handle owns B robots ("batch").  Host arrays are robot-major per quantity
+ *    (array[b * width + k]); each quantity is its own array (struct of arrays).
+ *  - Leg / joint order: LH, LF, RF, RH x (HAA, HFE, KFE) — the reference's model order
+ *    (cpp:81,234,327-341).  Contact bit i of contacts[b] = footContacts_[i] (cpp:183).
+ *  - base_pose[b] = (px, py, pz, qx, qy, qz, qw) as in gazebo_msgs/ModelStates.pose (cpp:209-218).
+ *  - nu[b] = (v_lin world (3), omega world (3), qdot (12)) = [baseVel_; jointVel_] (cpp:228,287).
+ *  - ref[b] = WbcReferenceMsg field order (msg/WbcReferenceMsg.msg:1-6): desiredComPose (6),
+ *    desiredComVelocity (6), desiredComAcceleration (6), desiredSwingLegsPosition (12),
+ *    desiredSwingLegsVelocity (12), desiredSwingLegsAcceleration (12).
+ *  - switching[b] = isSwitchingFootState_ (cpp:176-184); the caller latches it (quirk A.7).
+ *  - Every call returns WBC_OK (0) or a negative error; no exceptions cross the boundary.
+ *  - A handle is used by one host thread.  Inputs are snapshotted when the step kernel reads
+ *    them, which removes the reference's callback/control-thread race (cpp:499,681-682).
+ */
+#ifndef WBC_H
+#define WBC_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WBC_NUM_LEGS 4
+#define WBC_NUM_JOINTS 12
+#define WBC_NUM_DOF 18
+#define WBC_NV 42 /* qpNumberOfVariables, hpp:31 */
+#define WBC_NC 70 /* qpNumberOfConstraints, hpp:32 */
+#define WBC_POSE_LEN 7
+#define WBC_NU_LEN 18
+#define WBC_REF_LEN 54
+
+/* One lumped rigid body hanging off a revolute joint (tools/gen_model.py). */
+typedef struct wbc_link {
+    double R[9];       /* parent body frame -> joint frame at q = 0, row-major */
+    double p[3];       /* joint origin in the parent body frame */
+    double axis[3];    /* joint axis in the joint (= child body) frame */
+    double mass;
+    double com[3];     /* child body frame */
+    double inertia[9]; /* about the com, child body axes, row-major */
+} wbc_link;
+
+/* Lumped ANYmal model: replaces iDynTree::Model built from urdf/anymal.urdf (cpp:26-40). */
+typedef struct wbc_model {
+    double base_mass;
+    double base_com[3];
+    double base_inertia[9];
+    wbc_link link[WBC_NUM_LEGS][3]; /* legs LH, LF, RF, RH; links after HAA, HFE, KFE */
+    double foot[WBC_NUM_LEGS][3];   /* {LH,LF,RF,RH}_FOOT origin in the SHANK body frame */
+    double total_mass;              /* model_.getTotalMass(), cpp:72 */
+} wbc_model;
+
+/* Controller parameters: config/params_controller.yaml:1-12, read at cpp:122-148. */
+typedef struct wbc_params {
+    double friction;     /* mu */
+    double loop_rate;    /* Hz; finite-difference step 1/loop_rate (cpp:394) */
+    double max_torque;   /* torque limit rows R3 (cpp:506,513) */
+    double kp, kp_z, kd, ki;        /* wrench PD(I) gains (cpp:429-432) */
+    double kp_swing, kd_swing;      /* swing-foot PD (cpp:449-450) */
+    double slack_weight;            /* R block of slacks (cpp:476) */
+    double initial_reference_pose[6];
+    double gravity;                 /* gravityAcceleration, hpp:30 */
+    int32_t max_wsr;                /* nWSR = 100 (cpp:517) */
+    int32_t reserved;
+} wbc_params;
+
+/* API return codes. */
+enum {
+    WBC_OK = 0,
+    WBC_ERR_ARG = -1,
+    WBC_ERR_HIP = -2,
+    WBC_ERR_STATE = -3,
+    WBC_ERR_NO_DEVICE = -4
+};
+
+/* Per-robot QP status (status[] output); 0 mirrors qpOASES SUCCESSFUL_RETURN (cpp:654). */
+enum {
+    WBC_QP_OK = 0,
+    WBC_QP_MAX_ITER = 1,   /* more than max_wsr working-set changes (nWSR exceeded) */
+    WBC_QP_INFEASIBLE = 2, /* constraints inconsistent */
+    WBC_QP_NUMERIC = 3     /* non-finite input or factorisation breakdown */
+};
+
+/* Step flags. */
+#define WBC_STATELESS 1u /* cold step: history = reset values; history is neither read nor written */
+#define WBC_DEBUG 2u     /* also write the per-robot debug record (wbc_get_debug) */
+
+/* Debug record layout (doubles per robot), written by update/step under WBC_DEBUG. */
+enum {
+    WBC_DBG_COM = 0,        /* c (3)                       getCenterOfMassPosition (cpp:260) */
+    WBC_DBG_COMVEL = 3,     /* c-dot (3)                   getCenterOfMassVelocity (cpp:261) */
+    WBC_DBG_POSE = 6,       /* currentPose_ (6)            cpp:264 */
+    WBC_DBG_VC = 12,        /* centerOfMassVelocity_ (6)   cpp:261 */
+    WBC_DBG_M = 18,         /* mass matrix 18x18 row-major cpp:266 */
+    WBC_DBG_CNU = 342,      /* C(q,nu) nu (18)             cpp:544-551 */
+    WBC_DBG_JFEET = 360,    /* foot Jacobians rows 0-2, 12x18 (LH,LF,RF,RH) cpp:327-341 */
+    WBC_DBG_PFEET = 576,    /* foot positions (12)         cpp:344-362 */
+    WBC_DBG_VFEET = 588,    /* foot velocities (12)        cpp:364-382 */
+    WBC_DBG_MBARB = 600,    /* centroidMassMatrixBase_ 6x6 cpp:271 */
+    WBC_DBG_MBARJ = 636,    /* centroidMassMatrixJoints_ 12x12 cpp:272 */
+    WBC_DBG_JBAR = 780,     /* J_feet T^-1 (unmasked) 12x18 cpp:278-284 */
+    WBC_DBG_BBAR = 996,     /* centroidGeneralizedBias_ (18) cpp:289 */
+    WBC_DBG_WRENCH = 1014,  /* computeDesiredWrench (6)    cpp:426-445 */
+    WBC_DBG_R1 = 1020,      /* R1 bounds: -Jc_dot v (12)   cpp:504 */
+    WBC_DBG_RSW = 1032,     /* R4/R5 bound: cmd - Js_dot v (12) cpp:507,515 */
+    WBC_DBG_LEN = 1044
+};
+
+typedef struct wbc_engine wbc_engine;
+
+/* Defaults of config/params_controller.yaml and the lumped reference URDF. */
+int32_t wbc_default_params(wbc_params* out);
+int32_t wbc_anymal_model(wbc_model* out);
+
+int32_t wbc_create(const wbc_model* model, const wbc_params* params, int32_t batch, int32_t device,
+                   wbc_engine** out);
+int32_t wbc_destroy(wbc_engine* h);
+int32_t wbc_batch(const wbc_engine* h);
+/* Use a caller-owned hipStream_t (NULL = the engine's own stream). */
+int32_t wbc_set_stream(wbc_engine* h, void* hip_stream);
+
+/* Host inputs, copied to device on the engine stream. Any pointer may be NULL (= unchanged). */
+int32_t wbc_set_state(wbc_engine* h, const double* base_pose, const double* nu, const double* qj);
+int32_t wbc_set_reference(wbc_engine* h, const double* ref, const uint8_t* contacts,
+                          const uint8_t* switching);
+/* Device-resident inputs (no copy): the step reads these pointers directly.  NULL restores
+ * the engine-owned buffer for that quantity. */
+int32_t wbc_bind_device_inputs(wbc_engine* h, const double* d_base_pose, const double* d_nu,
+                               const double* d_qj, const double* d_ref, const uint8_t* d_contacts,
+                               const uint8_t* d_switching);
+
+/* Reset robots to setInitialState() (cpp:65-120) + first-iteration cold start.  mask NULL = all. */
+int32_t wbc_reset(wbc_engine* h, const uint8_t* mask);
+
+/* updateState(): dynamics, centroidal transform, finite differences, assembly (stream-ordered). */
+int32_t wbc_update(wbc_engine* h, uint32_t flags);
+/* solveQP() + computeJointTorques() on the problem assembled by the last wbc_update. */
+int32_t wbc_solve(wbc_engine* h, uint32_t flags);
+/* Fused update + solve + torques: the fast path. */
+int32_t wbc_step(wbc_engine* h, uint32_t flags);
+int32_t wbc_synchronize(wbc_engine* h);
+
+/* Outputs (host copies, synchronous).  Any pointer may be NULL.
+ * tau [B][12], grf [B][12] (= x[18:30]), x [B][42], status [B], iters [B]. */
+int32_t wbc_get_output(wbc_engine* h, double* tau, double* grf, double* x, int32_t* status,
+                       int32_t* iters);
+/* Device pointers of the output buffers (valid until wbc_destroy). */
+int32_t wbc_device_outputs(wbc_engine* h, double** d_tau, double** d_grf, double** d_x,
+                           int32_t** d_status, int32_t** d_iters);
+/* Debug records [B][WBC_DBG_LEN] of the last update/step run with WBC_DEBUG. */
+int32_t wbc_get_debug(wbc_engine* h, double* out);
+
+/* Launch statistics of the last wbc_step (ms, HIP events on the engine stream). */
+int32_t wbc_last_kernel_ms(wbc_engine* h, double* ms);
+const char* wbc_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WBC_H */

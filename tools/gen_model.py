@@ -1,0 +1,203 @@
+#!/usr/bin/env python3
+"""URDF -> lumped 13-body model constants for the batched WBC engine.
+
+The reference loads `urdf/anymal.urdf` through iDynTree's `ModelLoader::loadModelFromFile`
+(`src/whole_body_controller.cpp:26-40`) and lets `KinDynComputations` work on the full
+88-link tree.  Fixed joints carry no degrees of freedom, so every fixed child is rigidly
+lumped into the nearest ancestor that sits just after a revolute joint (or into the
+floating base).  That gives 13 rigid bodies: base + {HIP, THIGH, SHANK} x 4 legs.
+Lumping does not change M(q), C(q,v)v or any frame kinematics, so it is exact.
+
+Joint / leg order is an explicit model constant.  The reference assumes LH, LF, RF, RH
+(`src/whole_body_controller.cpp:81,234,327-341`, `config/controllers.yaml:7-19`); that is
+the default here.  Foot frames are `{LH,LF,RF,RH}_FOOT` (`src/whole_body_controller.cpp:327-379`).
+
+Outputs (committed, so nothing at run time reads /root/reference):
+  quadrupedwholebodycontroller_amd/model/anymal.json
+  include/wbc_anymal_model.h   (C initializer for `wbc_model`, see include/wbc.h)
+
+Usage:  python tools/gen_model.py [--urdf /root/reference/urdf/anymal.urdf]
+"""
+import argparse
+import json
+import math
+import os
+import xml.etree.ElementTree as ET
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LEG_ORDER = ["LH", "LF", "RF", "RH"]
+JOINT_SUFFIX = ["HAA", "HFE", "KFE"]
+
+
+def rpy_to_R(r, p, y):
+    """URDF convention: R = Rz(yaw) Ry(pitch) Rx(roll)."""
+    cr, sr = math.cos(r), math.sin(r)
+    cp, sp = math.cos(p), math.sin(p)
+    cy, sy = math.cos(y), math.sin(y)
+    Rx = np.array([[1, 0, 0], [0, cr, -sr], [0, sr, cr]])
+    Ry = np.array([[cp, 0, sp], [0, 1, 0], [-sp, 0, cp]])
+    Rz = np.array([[cy, -sy, 0], [sy, cy, 0], [0, 0, 1]])
+    return Rz @ Ry @ Rx
+
+
+def parse_origin(el):
+    if el is None:
+        return np.eye(3), np.zeros(3)
+    xyz = [float(v) for v in el.get("xyz", "0 0 0").split()]
+    rpy = [float(v) for v in el.get("rpy", "0 0 0").split()]
+    return rpy_to_R(*rpy), np.array(xyz)
+
+
+class Inertial:
+    """Mass, com and rotational inertia about the com, all in one frame."""
+
+    def __init__(self, m=0.0, c=None, I=None):
+        self.m = m
+        self.c = np.zeros(3) if c is None else c
+        self.I = np.zeros((3, 3)) if I is None else I
+
+    def transformed(self, R, p):
+        """Express in the parent frame, given child->parent rotation R and offset p."""
+        return Inertial(self.m, R @ self.c + p, R @ self.I @ R.T)
+
+    def __add__(self, o):
+        m = self.m + o.m
+        if m == 0.0:
+            return Inertial()
+        c = (self.m * self.c + o.m * o.c) / m
+
+        def shift(inr):
+            d = inr.c - c
+            return inr.I + inr.m * (np.dot(d, d) * np.eye(3) - np.outer(d, d))
+
+        return Inertial(m, c, shift(self) + shift(o))
+
+
+def load_urdf(path):
+    root = ET.parse(path).getroot()
+    links, joints = {}, {}
+    for el in root.findall("link"):
+        inert = el.find("inertial")
+        if inert is None:
+            links[el.get("name")] = Inertial()
+            continue
+        R, p = parse_origin(inert.find("origin"))
+        m = float(inert.find("mass").get("value"))
+        a = inert.find("inertia")
+        g = lambda k: float(a.get(k, "0"))
+        I = np.array([[g("ixx"), g("ixy"), g("ixz")],
+                      [g("ixy"), g("iyy"), g("iyz")],
+                      [g("ixz"), g("iyz"), g("izz")]])
+        links[el.get("name")] = Inertial(m, p, R @ I @ R.T)
+    for el in root.findall("joint"):
+        R, p = parse_origin(el.find("origin"))
+        ax = el.find("axis")
+        axis = np.array([float(v) for v in ax.get("xyz").split()]) if ax is not None else np.array([1.0, 0, 0])
+        joints[el.get("name")] = dict(type=el.get("type"), parent=el.find("parent").get("link"),
+                                      child=el.find("child").get("link"), R=R, p=p, axis=axis)
+    return links, joints
+
+
+def build(links, joints, leg_order=LEG_ORDER):
+    children = {}
+    for name, j in joints.items():
+        children.setdefault(j["parent"], []).append(name)
+    parents = {j["child"] for j in joints.values()}
+    roots = [l for l in links if l not in parents]
+    assert roots == ["base"], roots
+
+    def lump(link):
+        """Collect the rigid cluster rooted at `link`: its inertial, the revolute joints that
+        leave it (with their placement in `link`'s frame), and named frames inside it."""
+        inert = links[link]
+        out_joints, frames = [], {link: (np.eye(3), np.zeros(3))}
+        stack = [(link, np.eye(3), np.zeros(3))]
+        while stack:
+            lk, R, p = stack.pop()
+            for jn in children.get(lk, []):
+                j = joints[jn]
+                Rc, pc = R @ j["R"], R @ j["p"] + p
+                if j["type"] == "fixed":
+                    inert = inert + links[j["child"]].transformed(Rc, pc)
+                    frames[j["child"]] = (Rc, pc)
+                    stack.append((j["child"], Rc, pc))
+                else:
+                    assert j["type"] in ("revolute", "continuous"), j["type"]
+                    out_joints.append((jn, Rc, pc))
+        return inert, out_joints, frames
+
+    base_inert, base_out, _ = lump("base")
+    out_by_name = {jn: (Rc, pc) for jn, Rc, pc in base_out}
+    model = dict(base=dict(mass=base_inert.m, com=base_inert.c.tolist(), inertia=base_inert.I.tolist()),
+                 legs=[], leg_order=list(leg_order), joint_names=[], foot_names=[])
+    total = base_inert.m
+    for leg in leg_order:
+        jn = f"{leg}_{JOINT_SUFFIX[0]}"
+        Rc, pc = out_by_name[jn]
+        leg_links = []
+        for k in range(3):
+            j = joints[jn]
+            inert, outs, frames = lump(j["child"])
+            total += inert.m
+            leg_links.append(dict(joint=jn, R=Rc.tolist(), p=pc.tolist(), axis=j["axis"].tolist(),
+                                  mass=inert.m, com=inert.c.tolist(), inertia=inert.I.tolist(),
+                                  body=j["child"]))
+            model["joint_names"].append(jn)
+            if k < 2:
+                nxt = f"{leg}_{JOINT_SUFFIX[k + 1]}"
+                match = [o for o in outs if o[0] == nxt]
+                assert len(match) == 1, (nxt, [o[0] for o in outs])
+                jn, Rc, pc = match[0]
+            else:
+                assert not outs
+                foot = f"{leg}_FOOT"
+                model["foot_names"].append(foot)
+                model.setdefault("foot", []).append(frames[foot][1].tolist())
+        model["legs"].append(leg_links)
+    model["total_mass"] = total
+    return model
+
+
+def c_header(model):
+    def arr(v):
+        return "{" + ", ".join(repr(float(x)) for x in np.asarray(v).ravel()) + "}"
+
+    lines = ["/* Generated by tools/gen_model.py from the reference's urdf/anymal.urdf. Do not edit. */",
+             "#ifndef WBC_ANYMAL_MODEL_H", "#define WBC_ANYMAL_MODEL_H", '#include "wbc.h"', "",
+             "/* Leg order: " + ", ".join(model["leg_order"]) + "; joints per leg HAA, HFE, KFE. */",
+             "static const wbc_model WBC_ANYMAL_MODEL = {",
+             f"  {model['base']['mass']!r}, {arr(model['base']['com'])}, {arr(model['base']['inertia'])},",
+             "  {"]
+    for leg in model["legs"]:
+        lines.append("    {")
+        for lk in leg:
+            lines.append(f"      {{{arr(lk['R'])}, {arr(lk['p'])}, {arr(lk['axis'])}, {lk['mass']!r}, "
+                         f"{arr(lk['com'])}, {arr(lk['inertia'])}}},")
+        lines.append("    },")
+    lines.append("  },")
+    lines.append("  {" + ", ".join(arr(f) for f in model["foot"]) + "},")
+    lines.append(f"  {model['total_mass']!r}")
+    lines.append("};")
+    lines.append("#endif")
+    return "\n".join(lines) + "\n"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--urdf", default="/root/reference/urdf/anymal.urdf")
+    args = ap.parse_args()
+    links, joints = load_urdf(args.urdf)
+    model = build(links, joints)
+    model["source"] = "reference urdf/anymal.urdf (lumped by tools/gen_model.py)"
+    with open(os.path.join(REPO, "quadrupedwholebodycontroller_amd", "model", "anymal.json"), "w") as f:
+        json.dump(model, f, indent=1)
+    with open(os.path.join(REPO, "include", "wbc_anymal_model.h"), "w") as f:
+        f.write(c_header(model))
+    print("total mass", model["total_mass"], "base", model["base"]["mass"],
+          [[lk["mass"] for lk in leg] for leg in model["legs"]][0])
+
+
+if __name__ == "__main__":
+    main()
