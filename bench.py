@@ -1,0 +1,242 @@
+#!/usr/bin/env python3
+"""Benchmark: batched ANYmal WBC QP solves/s on MI355X (BASELINE.json metric).
+
+One step = one wbc_step over the rank's batch (dynamics + centroidal assembly + QP + torques,
+one fused HIP kernel), plus for N > 1 the RCCL all-gather of the torque block.  Inputs are
+resident in HBM before the timed region.  Default workload: configs[1] of BASELINE.json,
+B = 4096 four-contact stance states, cold solves, per GPU (weak scaling).
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under torch.distributed.run.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP64_PEAK_TFLOPS = 78.6   # MI355X fp64 dense peak (vector = matrix on gfx950; AMD spec, = 1/2 of 157.3 TF fp32)
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+# algorithmic flops per solve F(k) = F_dyn + F_asm + F_tau + F_fact + k F_iter
+F_DYN, F_ASM, F_TAU, F_FACT, F_ITER = 9000, 14000, 600, 24696, 12936
+BYTES_COLD = 929          # 729 B in + 200 B out per cold solve
+
+CONFIGS = {
+    "stance_cold_b4096": dict(gen="stance_cold", batch=4096, seed=1,
+                              desc="BASELINE configs[1]: B=4096 4-contact stance QPs, fp64, cold start"),
+    "rl_random_b8192": dict(gen="rl_random", batch=8192, seed=3,
+                            desc="BASELINE configs[3] per-GPU shard: randomized q/qd, 16 contact masks, cold"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(inp, budget_s=15.0):
+    """Time the CPU restatement of the reference path (oracle) on a bounded sample, 1 core."""
+    import ctypes
+
+    lib_path = os.path.join(ROOT, "oracle", "_build", "libwbc_ref.so")
+    B = inp["base_pose"].shape[0]
+    if os.path.exists(lib_path):
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import wbc_ref  # ctypes wrapper of the C restatement
+
+        n = 1
+        t_used = 0.0
+        while True:
+            idx = np.arange(n) % B
+            sub = {k: np.ascontiguousarray(v[idx]) for k, v in inp.items()}
+            t0 = time.perf_counter()
+            wbc_ref.run_batch(sub)
+            dt = time.perf_counter() - t0
+            t_used += dt
+            if dt >= budget_s / 4 or t_used >= budget_s:
+                break
+            n = int(n * max(2.0, min(10.0, (budget_s / 4) / max(dt, 1e-6))))
+        return dict(value=n / dt, unit="solves/s", cores=1, kind="port",
+                    sample=f"{n} cold solves of the same workload through oracle/wbc_ref.c "
+                           f"(dense reference-faithful restatement, -O3), 1 thread, {dt:.2f} s")
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import wbc_np as W
+
+    model, params = W.Model(), W.default_params()
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s and n < B:
+        c = W.ReferenceWBC(model, params)
+        c.set_state(inp["base_pose"][n], inp["nu"][n], inp["qj"][n])
+        c.set_reference(inp["ref"][n], [(int(inp["contacts"][n]) >> i) & 1 for i in range(4)], True)
+        c.step()
+        n += 1
+    dt = time.perf_counter() - t0
+    return dict(value=n / dt, unit="solves/s", cores=1, kind="port",
+                sample=f"{n} cold solves through oracle/wbc_np.py (numpy restatement), 1 thread, {dt:.2f} s")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="stance_cold_b4096", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=0, help="override per-GPU batch")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--extra", action="store_true", help="also time the other configs (reported under 'extra')")
+    args = ap.parse_args()
+
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(local_rank)
+
+    from quadrupedwholebodycontroller_amd import STATELESS, Engine, workloads
+
+    cfg = CONFIGS[args.config]
+    B = args.batch or cfg["batch"]
+    gen = getattr(workloads, cfg["gen"])
+    inp = gen(B, seed=cfg["seed"] + 1000 * rank)
+
+    stream = torch.cuda.current_stream()
+    e = Engine(B, device=local_rank)
+    e.set_stream(stream.cuda_stream)
+    e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
+    e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
+    tau_local = torch.zeros(B * 12, dtype=torch.float64, device="cuda")
+    e.bind_device_outputs(tau=tau_local.data_ptr())
+    tau_all = torch.zeros(world * B * 12, dtype=torch.float64, device="cuda") if world > 1 else None
+
+    def one_step():
+        e.step(STATELESS)
+        if world > 1:
+            dist.all_gather_into_tensor(tau_all, tau_local)
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    # kernel-only timing with HIP events on the launch stream (for the roofline)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for _ in range(args.steps):
+        e.step(STATELESS)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    out = e.outputs()
+    iters = out["iters"].astype(np.int64)
+    status = out["status"]
+    flops = float(np.sum(F_DYN + F_ASM + F_TAU + F_FACT + F_ITER * iters))
+    achieved_tf = flops / (kernel_ms * 1e-3) / 1e12
+    hbm_gbs = B * BYTES_COLD / (kernel_ms * 1e-3) / 1e9
+
+    extra = {}
+    if args.extra and rank == 0:
+        for name, c2 in CONFIGS.items():
+            if name == args.config:
+                continue
+            B2 = c2["batch"]
+            inp2 = getattr(workloads, c2["gen"])(B2, seed=c2["seed"])
+            e2 = Engine(B2, device=local_rank)
+            e2.set_stream(stream.cuda_stream)
+            e2.set_state(inp2["base_pose"], inp2["nu"], inp2["qj"])
+            e2.set_reference(inp2["ref"], inp2["contacts"], inp2["switching"])
+            for _ in range(args.warmup):
+                e2.step(STATELESS)
+            ev0.record(stream)
+            for _ in range(args.steps):
+                e2.step(STATELESS)
+            ev1.record(stream)
+            torch.cuda.synchronize()
+            ms2 = ev0.elapsed_time(ev1) / args.steps
+            o2 = e2.outputs()
+            extra[name] = dict(batch=B2, ms_per_step=ms2, solves_per_s=B2 / (ms2 * 1e-3),
+                               status_counts=np.bincount(o2["status"], minlength=4).tolist(),
+                               mean_iters=float(o2["iters"].mean()), desc=c2["desc"])
+            e2.close()
+
+    total = B * world * args.steps
+    value = total / elapsed
+    result = {
+        "metric": "WBC QP solves/sec (ANYmal 18-DoF, 4-contact) at 1/2/4/8 GPUs; % HBM roofline",
+        "value": value,
+        "unit": "solves/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (SURVEY.md 8d generators, numpy PCG64 seed %d + 1000*rank)" % cfg["seed"],
+        "config": {"workload": args.config, "description": cfg["desc"], "batch_per_gpu": B,
+                   "global_batch": B * world, "parallelism": f"dp{world} (robot shards) + RCCL all-gather of tau"
+                   if world > 1 else "dp1"},
+        "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": None,
+                     "kernel": "wbc_step_kernel", "kernel_ms": kernel_ms,
+                     "note": "fp64 compute roof (gfx950 fp64 vector = matrix peak); algorithmic flops F(k) of "
+                             "SURVEY 8(d), k = iters[] per robot; the path is latency-bound, not HBM-bound"},
+        "roofline_hbm": {"bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": hbm_gbs / HBM_PEAK_GBS, "bytes_per_solve": BYTES_COLD},
+        "qp_status_counts": np.bincount(status, minlength=4).tolist(),
+        "mean_iters": float(iters.mean()),
+    }
+    if extra:
+        result["extra"] = extra
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(inp, args.cpu_budget)
+        import multiprocessing
+
+        result["cpu_baseline"]["host"] = dict(nproc=multiprocessing.cpu_count(), model=_cpu_model())
+    e.close()
+    if world > 1:
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+if __name__ == "__main__":
+    main()

@@ -150,6 +150,11 @@ int32_t wbc_bind_device_inputs(wbc_engine* h, const double* d_base_pose, const d
                                const double* d_qj, const double* d_ref, const uint8_t* d_contacts,
                                const uint8_t* d_switching);
 
+/* Caller-owned device output buffers (no copy): the step writes into these pointers directly
+ * (e.g. a tensor that an RCCL all-gather then reads).  NULL restores the engine-owned buffer. */
+int32_t wbc_bind_device_outputs(wbc_engine* h, double* d_tau, double* d_grf, double* d_x, int32_t* d_status,
+                                int32_t* d_iters);
+
 /* Reset robots to setInitialState() (cpp:65-120) + first-iteration cold start.  mask NULL = all. */
 int32_t wbc_reset(wbc_engine* h, const uint8_t* mask);
 

@@ -1,0 +1,17 @@
+"""quadrupedwholebodycontroller_amd — MI355X-native batched whole-body-control QP engine.
+
+The hot path of the reference's `WholeBodyController` (updateState -> solveQP ->
+computeJointTorques, src/whole_body_controller.cpp:650-652) as hand-written HIP for gfx950,
+behind the C-ABI in include/wbc.h.  This package is the Python view of that C-ABI:
+
+  Engine          batched handle (wbc_create ... wbc_get_output), see _capi.py
+  workloads       synthetic inputs of the BASELINE.json configurations
+  controller      WholeBodyController-shaped single-robot shim over the engine
+
+The product path has no CPU fallback: without libwbc_hip.so or a GPU it raises.
+"""
+from ._capi import (DEBUG, STATELESS, QP_INFEASIBLE, QP_MAX_ITER, QP_NUMERIC, QP_OK, Engine, WbcError,  # noqa: F401
+                    WbcModel, WbcParams, anymal_model, default_params, load_library, split_debug)
+
+__all__ = ["Engine", "WbcError", "WbcModel", "WbcParams", "anymal_model", "default_params", "load_library",
+           "split_debug", "STATELESS", "DEBUG", "QP_OK", "QP_MAX_ITER", "QP_INFEASIBLE", "QP_NUMERIC"]

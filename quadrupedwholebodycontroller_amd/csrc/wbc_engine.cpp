@@ -1,0 +1,382 @@
+// wbc_engine.cpp — host side of the C-ABI (include/wbc.h): device buffers, stream ordering,
+// kernel launches.  Replaces the per-object state of the reference's WholeBodyController
+// (include/anymal_wbc/whole_body_controller.hpp:106-166) with batched device buffers.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "wbc.h"
+#include "wbc_anymal_model.h"
+#include "wbc_layout.h"
+
+
+extern "C" hipError_t wbc_launch_step(const wbc::KernelArgs* a, hipStream_t st);
+extern "C" hipError_t wbc_launch_update(const wbc::KernelArgs* a, hipStream_t st);
+extern "C" hipError_t wbc_launch_solve(const wbc::KernelArgs* a, hipStream_t st);
+extern "C" hipError_t wbc_launch_reset(double* hist, const uint8_t* mask, int batch, hipStream_t st);
+
+namespace {
+thread_local std::string g_err;
+
+int32_t fail(int32_t code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+#define WBC_HIP(call)                                                                         \
+    do {                                                                                      \
+        hipError_t e_ = (call);                                                               \
+        if (e_ != hipSuccess) return fail(WBC_ERR_HIP, std::string(#call ": ") + hipGetErrorString(e_)); \
+    } while (0)
+}  // namespace
+
+struct wbc_engine {
+    int32_t batch = 0;
+    int32_t device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    wbc_model* d_model = nullptr;
+    wbc_params* d_params = nullptr;
+    // owned inputs
+    double* d_pose = nullptr;
+    double* d_nu = nullptr;
+    double* d_qj = nullptr;
+    double* d_ref = nullptr;
+    uint8_t* d_contacts = nullptr;
+    uint8_t* d_switching = nullptr;
+    uint8_t* d_mask = nullptr;
+    // bound (possibly external) inputs
+    const double* in_pose = nullptr;
+    const double* in_nu = nullptr;
+    const double* in_qj = nullptr;
+    const double* in_ref = nullptr;
+    const uint8_t* in_contacts = nullptr;
+    const uint8_t* in_switching = nullptr;
+    // state / outputs
+    double* d_hist = nullptr;
+    double* d_work = nullptr;
+    double* d_tau = nullptr;
+    double* d_grf = nullptr;
+    double* d_x = nullptr;
+    int32_t* d_status = nullptr;
+    int32_t* d_iters = nullptr;
+    double* d_dbg = nullptr;
+    // bound (possibly external) outputs
+    double* out_tau = nullptr;
+    double* out_grf = nullptr;
+    double* out_x = nullptr;
+    int32_t* out_status = nullptr;
+    int32_t* out_iters = nullptr;
+    bool updated = false;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double last_ms = 0.0;
+};
+
+namespace {
+template <class T>
+hipError_t dalloc(T** p, size_t n) {
+    return hipMalloc(reinterpret_cast<void**>(p), sizeof(T) * (n ? n : 1));
+}
+
+wbc::KernelArgs make_args(wbc_engine* h, uint32_t flags) {
+    wbc::KernelArgs a;
+    a.model = h->d_model;
+    a.params = h->d_params;
+    a.base_pose = h->in_pose;
+    a.nu = h->in_nu;
+    a.qj = h->in_qj;
+    a.ref = h->in_ref;
+    a.contacts = h->in_contacts;
+    a.switching = h->in_switching;
+    a.hist = h->d_hist;
+    a.work = h->d_work;
+    a.tau = h->out_tau;
+    a.grf = h->out_grf;
+    a.x = h->out_x;
+    a.status = h->out_status;
+    a.iters = h->out_iters;
+    a.dbg = h->d_dbg;
+    a.batch = h->batch;
+    a.stateful = (flags & WBC_STATELESS) ? 0 : 1;
+    a.debug = (flags & WBC_DEBUG) ? 1 : 0;
+    return a;
+}
+}  // namespace
+
+extern "C" {
+
+int32_t wbc_default_params(wbc_params* p) {
+    if (!p) return fail(WBC_ERR_ARG, "null params");
+    std::memset(p, 0, sizeof(*p));
+    p->friction = 1.0;       // params_controller.yaml:2
+    p->loop_rate = 400.0;    // :3
+    p->max_torque = 80.0;    // :4
+    p->kp = 6000.0;          // :5
+    p->kp_z = 10000.0;       // :6
+    p->kd = 1800.0;          // :7
+    p->ki = 0.0;             // :8
+    p->kp_swing = 250.0;     // :9
+    p->kd_swing = 20.0;      // :10
+    p->slack_weight = 1000.0;  // :11
+    const double pose[6] = {0.0, 0.0, 0.50, 0.0, 0.0, 0.0};  // :12
+    std::memcpy(p->initial_reference_pose, pose, sizeof(pose));
+    p->gravity = 9.81;       // hpp:30
+    p->max_wsr = 100;        // cpp:517
+    return WBC_OK;
+}
+
+int32_t wbc_anymal_model(wbc_model* m) {
+    if (!m) return fail(WBC_ERR_ARG, "null model");
+    *m = WBC_ANYMAL_MODEL;
+    return WBC_OK;
+}
+
+int32_t wbc_create(const wbc_model* model, const wbc_params* params, int32_t batch, int32_t device, wbc_engine** out) {
+    if (!out || batch <= 0) return fail(WBC_ERR_ARG, "wbc_create: bad arguments");
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(WBC_ERR_NO_DEVICE, "no HIP device");
+    if (device < 0 || device >= ndev) return fail(WBC_ERR_ARG, "wbc_create: bad device index");
+    WBC_HIP(hipSetDevice(device));
+    wbc_engine* h = new (std::nothrow) wbc_engine();
+    if (!h) return fail(WBC_ERR_ARG, "out of host memory");
+    h->batch = batch;
+    h->device = device;
+    wbc_model m = model ? *model : WBC_ANYMAL_MODEL;
+    wbc_params p;
+    if (params) p = *params;
+    else wbc_default_params(&p);
+    if (p.loop_rate <= 0.0 || p.max_wsr <= 0) {
+        delete h;
+        return fail(WBC_ERR_ARG, "wbc_create: invalid params");
+    }
+    const size_t B = (size_t)batch;
+#define ALLOC(ptr, n)                                             \
+    if (dalloc(&h->ptr, (n)) != hipSuccess) {                     \
+        wbc_destroy(h);                                           \
+        return fail(WBC_ERR_HIP, "hipMalloc failed: " #ptr);      \
+    }
+    ALLOC(d_model, 1);
+    ALLOC(d_params, 1);
+    ALLOC(d_pose, B * WBC_POSE_LEN);
+    ALLOC(d_nu, B * WBC_NU_LEN);
+    ALLOC(d_qj, B * WBC_NUM_JOINTS);
+    ALLOC(d_ref, B * WBC_REF_LEN);
+    ALLOC(d_contacts, B);
+    ALLOC(d_switching, B);
+    ALLOC(d_mask, B);
+    ALLOC(d_hist, B * wbc::HIST_LEN);
+    ALLOC(d_work, B * wbc::PROB_LEN);
+    ALLOC(d_tau, B * WBC_NUM_JOINTS);
+    ALLOC(d_grf, B * WBC_NUM_JOINTS);
+    ALLOC(d_x, B * WBC_NV);
+    ALLOC(d_status, B);
+    ALLOC(d_iters, B);
+    ALLOC(d_dbg, B * WBC_DBG_LEN);
+#undef ALLOC
+    if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) {
+        wbc_destroy(h);
+        return fail(WBC_ERR_HIP, "stream/event creation failed");
+    }
+    h->stream = h->own_stream;
+    h->in_pose = h->d_pose;
+    h->in_nu = h->d_nu;
+    h->in_qj = h->d_qj;
+    h->in_ref = h->d_ref;
+    h->in_contacts = h->d_contacts;
+    h->in_switching = h->d_switching;
+    h->out_tau = h->d_tau;
+    h->out_grf = h->d_grf;
+    h->out_x = h->d_x;
+    h->out_status = h->d_status;
+    h->out_iters = h->d_iters;
+    hipStream_t st = h->stream;
+    if (hipMemcpyAsync(h->d_model, &m, sizeof(m), hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(h->d_params, &p, sizeof(p), hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemsetAsync(h->d_pose, 0, B * WBC_POSE_LEN * sizeof(double), st) != hipSuccess ||
+        hipMemsetAsync(h->d_nu, 0, B * WBC_NU_LEN * sizeof(double), st) != hipSuccess ||
+        hipMemsetAsync(h->d_qj, 0, B * WBC_NUM_JOINTS * sizeof(double), st) != hipSuccess ||
+        hipMemsetAsync(h->d_ref, 0, B * WBC_REF_LEN * sizeof(double), st) != hipSuccess ||
+        hipMemsetAsync(h->d_contacts, 15, B, st) != hipSuccess ||
+        hipMemsetAsync(h->d_switching, 0, B, st) != hipSuccess ||
+        hipMemsetAsync(h->d_status, 0, B * sizeof(int32_t), st) != hipSuccess ||
+        hipMemsetAsync(h->d_iters, 0, B * sizeof(int32_t), st) != hipSuccess ||
+        hipMemsetAsync(h->d_tau, 0, B * WBC_NUM_JOINTS * sizeof(double), st) != hipSuccess ||
+        hipMemsetAsync(h->d_grf, 0, B * WBC_NUM_JOINTS * sizeof(double), st) != hipSuccess ||
+        hipMemsetAsync(h->d_x, 0, B * WBC_NV * sizeof(double), st) != hipSuccess ||
+        hipMemsetAsync(h->d_dbg, 0, B * WBC_DBG_LEN * sizeof(double), st) != hipSuccess ||
+        wbc_launch_reset(h->d_hist, nullptr, batch, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+        wbc_destroy(h);
+        return fail(WBC_ERR_HIP, "wbc_create: initialisation failed");
+    }
+    *out = h;
+    return WBC_OK;
+}
+
+int32_t wbc_destroy(wbc_engine* h) {
+    if (!h) return WBC_OK;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    void* ptrs[] = {h->d_model, h->d_params, h->d_pose, h->d_nu, h->d_qj, h->d_ref, h->d_contacts, h->d_switching,
+                    h->d_mask, h->d_hist, h->d_work, h->d_tau, h->d_grf, h->d_x, h->d_status, h->d_iters, h->d_dbg};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    if (h->ev0) (void)hipEventDestroy(h->ev0);
+    if (h->ev1) (void)hipEventDestroy(h->ev1);
+    if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
+    delete h;
+    return WBC_OK;
+}
+
+int32_t wbc_batch(const wbc_engine* h) { return h ? h->batch : 0; }
+
+int32_t wbc_set_stream(wbc_engine* h, void* stream) {
+    if (!h) return fail(WBC_ERR_ARG, "null handle");
+    h->stream = stream ? reinterpret_cast<hipStream_t>(stream) : h->own_stream;
+    return WBC_OK;
+}
+
+int32_t wbc_set_state(wbc_engine* h, const double* base_pose, const double* nu, const double* qj) {
+    if (!h) return fail(WBC_ERR_ARG, "null handle");
+    WBC_HIP(hipSetDevice(h->device));
+    const size_t B = (size_t)h->batch;
+    if (base_pose) { WBC_HIP(hipMemcpyAsync(h->d_pose, base_pose, B * WBC_POSE_LEN * sizeof(double), hipMemcpyHostToDevice, h->stream)); h->in_pose = h->d_pose; }
+    if (nu) { WBC_HIP(hipMemcpyAsync(h->d_nu, nu, B * WBC_NU_LEN * sizeof(double), hipMemcpyHostToDevice, h->stream)); h->in_nu = h->d_nu; }
+    if (qj) { WBC_HIP(hipMemcpyAsync(h->d_qj, qj, B * WBC_NUM_JOINTS * sizeof(double), hipMemcpyHostToDevice, h->stream)); h->in_qj = h->d_qj; }
+    WBC_HIP(hipStreamSynchronize(h->stream));  // host buffers may be reused by the caller
+    return WBC_OK;
+}
+
+int32_t wbc_set_reference(wbc_engine* h, const double* ref, const uint8_t* contacts, const uint8_t* switching) {
+    if (!h) return fail(WBC_ERR_ARG, "null handle");
+    WBC_HIP(hipSetDevice(h->device));
+    const size_t B = (size_t)h->batch;
+    if (ref) { WBC_HIP(hipMemcpyAsync(h->d_ref, ref, B * WBC_REF_LEN * sizeof(double), hipMemcpyHostToDevice, h->stream)); h->in_ref = h->d_ref; }
+    if (contacts) { WBC_HIP(hipMemcpyAsync(h->d_contacts, contacts, B, hipMemcpyHostToDevice, h->stream)); h->in_contacts = h->d_contacts; }
+    if (switching) { WBC_HIP(hipMemcpyAsync(h->d_switching, switching, B, hipMemcpyHostToDevice, h->stream)); h->in_switching = h->d_switching; }
+    WBC_HIP(hipStreamSynchronize(h->stream));
+    return WBC_OK;
+}
+
+int32_t wbc_bind_device_inputs(wbc_engine* h, const double* d_base_pose, const double* d_nu, const double* d_qj,
+                               const double* d_ref, const uint8_t* d_contacts, const uint8_t* d_switching) {
+    if (!h) return fail(WBC_ERR_ARG, "null handle");
+    h->in_pose = d_base_pose ? d_base_pose : h->d_pose;
+    h->in_nu = d_nu ? d_nu : h->d_nu;
+    h->in_qj = d_qj ? d_qj : h->d_qj;
+    h->in_ref = d_ref ? d_ref : h->d_ref;
+    h->in_contacts = d_contacts ? d_contacts : h->d_contacts;
+    h->in_switching = d_switching ? d_switching : h->d_switching;
+    return WBC_OK;
+}
+
+int32_t wbc_bind_device_outputs(wbc_engine* h, double* d_tau, double* d_grf, double* d_x, int32_t* d_status,
+                                int32_t* d_iters) {
+    if (!h) return fail(WBC_ERR_ARG, "null handle");
+    h->out_tau = d_tau ? d_tau : h->d_tau;
+    h->out_grf = d_grf ? d_grf : h->d_grf;
+    h->out_x = d_x ? d_x : h->d_x;
+    h->out_status = d_status ? d_status : h->d_status;
+    h->out_iters = d_iters ? d_iters : h->d_iters;
+    return WBC_OK;
+}
+
+int32_t wbc_reset(wbc_engine* h, const uint8_t* mask) {
+    if (!h) return fail(WBC_ERR_ARG, "null handle");
+    WBC_HIP(hipSetDevice(h->device));
+    const uint8_t* dm = nullptr;
+    if (mask) {
+        WBC_HIP(hipMemcpyAsync(h->d_mask, mask, (size_t)h->batch, hipMemcpyHostToDevice, h->stream));
+        dm = h->d_mask;
+    }
+    WBC_HIP(wbc_launch_reset(h->d_hist, dm, h->batch, h->stream));
+    WBC_HIP(hipStreamSynchronize(h->stream));
+    h->updated = false;
+    return WBC_OK;
+}
+
+int32_t wbc_update(wbc_engine* h, uint32_t flags) {
+    if (!h) return fail(WBC_ERR_ARG, "null handle");
+    WBC_HIP(hipSetDevice(h->device));
+    wbc::KernelArgs a = make_args(h, flags);
+    WBC_HIP(wbc_launch_update(&a, h->stream));
+    h->updated = true;
+    return WBC_OK;
+}
+
+int32_t wbc_solve(wbc_engine* h, uint32_t flags) {
+    if (!h) return fail(WBC_ERR_ARG, "null handle");
+    if (!h->updated) return fail(WBC_ERR_STATE, "wbc_solve before wbc_update");
+    WBC_HIP(hipSetDevice(h->device));
+    wbc::KernelArgs a = make_args(h, flags);
+    WBC_HIP(wbc_launch_solve(&a, h->stream));
+    h->updated = false;
+    return WBC_OK;
+}
+
+int32_t wbc_step(wbc_engine* h, uint32_t flags) {
+    if (!h) return fail(WBC_ERR_ARG, "null handle");
+    WBC_HIP(hipSetDevice(h->device));
+    wbc::KernelArgs a = make_args(h, flags);
+    WBC_HIP(hipEventRecord(h->ev0, h->stream));
+    WBC_HIP(wbc_launch_step(&a, h->stream));
+    WBC_HIP(hipEventRecord(h->ev1, h->stream));
+    h->updated = false;
+    return WBC_OK;
+}
+
+int32_t wbc_synchronize(wbc_engine* h) {
+    if (!h) return fail(WBC_ERR_ARG, "null handle");
+    WBC_HIP(hipSetDevice(h->device));
+    WBC_HIP(hipStreamSynchronize(h->stream));
+    return WBC_OK;
+}
+
+int32_t wbc_get_output(wbc_engine* h, double* tau, double* grf, double* x, int32_t* status, int32_t* iters) {
+    if (!h) return fail(WBC_ERR_ARG, "null handle");
+    WBC_HIP(hipSetDevice(h->device));
+    const size_t B = (size_t)h->batch;
+    hipStream_t st = h->stream;
+    if (tau) WBC_HIP(hipMemcpyAsync(tau, h->out_tau, B * 12 * sizeof(double), hipMemcpyDeviceToHost, st));
+    if (grf) WBC_HIP(hipMemcpyAsync(grf, h->out_grf, B * 12 * sizeof(double), hipMemcpyDeviceToHost, st));
+    if (x) WBC_HIP(hipMemcpyAsync(x, h->out_x, B * WBC_NV * sizeof(double), hipMemcpyDeviceToHost, st));
+    if (status) WBC_HIP(hipMemcpyAsync(status, h->out_status, B * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    if (iters) WBC_HIP(hipMemcpyAsync(iters, h->out_iters, B * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    WBC_HIP(hipStreamSynchronize(st));
+    return WBC_OK;
+}
+
+int32_t wbc_device_outputs(wbc_engine* h, double** d_tau, double** d_grf, double** d_x, int32_t** d_status,
+                           int32_t** d_iters) {
+    if (!h) return fail(WBC_ERR_ARG, "null handle");
+    if (d_tau) *d_tau = h->out_tau;
+    if (d_grf) *d_grf = h->out_grf;
+    if (d_x) *d_x = h->out_x;
+    if (d_status) *d_status = h->out_status;
+    if (d_iters) *d_iters = h->out_iters;
+    return WBC_OK;
+}
+
+int32_t wbc_get_debug(wbc_engine* h, double* out) {
+    if (!h || !out) return fail(WBC_ERR_ARG, "null argument");
+    WBC_HIP(hipSetDevice(h->device));
+    WBC_HIP(hipMemcpyAsync(out, h->d_dbg, (size_t)h->batch * WBC_DBG_LEN * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    WBC_HIP(hipStreamSynchronize(h->stream));
+    return WBC_OK;
+}
+
+int32_t wbc_last_kernel_ms(wbc_engine* h, double* ms) {
+    if (!h || !ms) return fail(WBC_ERR_ARG, "null argument");
+    float f = 0.f;
+    WBC_HIP(hipEventSynchronize(h->ev1));
+    WBC_HIP(hipEventElapsedTime(&f, h->ev0, h->ev1));
+    *ms = (double)f;
+    return WBC_OK;
+}
+
+const char* wbc_last_error(void) { return g_err.c_str(); }
+
+}  // extern "C"

@@ -1,0 +1,1205 @@
+// wbc_kernel.hip — batched whole-body-control step for gfx950 (MI355X), fp64.
+//
+// One robot per 64-lane wavefront (one workgroup = one wave).  Phases, each a device function
+// over the robot's LDS record:
+//
+//   update (≙ WholeBodyController::updateState, src/whole_body_controller.cpp:256-294)
+//     lanes 0..12 = rigid bodies: forward kinematics, body velocities, Newton-Euler bias terms
+//     (iDynTree KinDynComputations in MIXED representation, cpp:258-266,327-379,544-551);
+//     lanes 0..11 = joints: centroidal momentum matrix columns, leg blocks of M, joint bias;
+//     closed forms of T^-1, Mbar = T^-T M T^-1, Jbar = J T^-1, bbar (cpp:268-293) instead of the
+//     reference's seven dense 18x18 LU inverses; finite differences against the HBM history
+//     (computeDerivatives, cpp:384-402); desired wrench and swing commands (cpp:426-464).
+//   solve (≙ solveQP + computeJointTorques, cpp:466-577)
+//     The 42-variable / 70-row QP is reduced exactly to 24 variables and
+//     solved with the Goldfarb-Idnani dual active-set method: lane p owns constraint p and
+//     its column C[:,p] = J^T n_p (J = L^-T Q), so every product the method needs is lane-local;
+//     R^-1 (packed) lives in LDS; Householder reflections add constraints, Givens rotations drop
+//     them.  The primal solution is recovered from the final multipliers (x = x0 + H^-1 N u).
+//
+// Nothing here is wave-size agnostic: 64-lane waves are assumed (gfx950).
+#include <hip/hip_runtime.h>
+
+#include "wbc.h"
+#include "wbc_layout.h"
+
+namespace wbc {
+
+#ifndef WBC_WAVES_PER_SIMD
+#define WBC_WAVES_PER_SIMD 1
+#endif
+constexpr int NQ = 24;                 // reduced QP variables
+constexpr int RPACK = NQ * (NQ + 1) / 2;
+
+
+struct UpdScratch {
+    double in[92];          // pose 7 | nu 18 | q 12 | ref 54
+    double bc[13][3];       // body com (world)
+    double bI[13][9];       // body inertia about com (world)
+    double bm[13];
+    double bw[13][3];       // body angular velocity
+    double bF[13][3];       // m * com acceleration at nu_dot = 0
+    double bN[13][3];       // I alpha + w x I w
+    double bv[13][3];       // com velocity
+    double ja[12][3];       // joint axis (world)
+    double jo[12][3];       // joint origin (world)
+    double pf[4][3];
+    double vf[4][3];
+    double Jf[4][9];        // foot Jacobian joint columns of its leg: [row r][k]
+    double A[12][6];        // centroidal momentum matrix joint columns (lin 3, ang about c 3)
+    double KA[12][3];       // I_c^-1 A_ang
+    double Mjj[12][3];      // leg block rows of M
+    double hj[12];          // joint bias (C nu)_j
+    double contrib[13][6];  // per-body partial sums
+    double cen[40];         // uniform scratch (see CEN_*)
+};
+
+struct QpScratch {
+    double Hs[12][13];   // slot Hessian, Cholesky in place (lower)
+    double Linv[12][13]; // L^-1
+    double gs[12];
+    double xs[12];       // slot part of x0 = -H^-1 g
+    double tmp[12];
+    double Rinv[RPACK];  // packed upper-triangular R^-1, column-major: (i,j) -> j(j+1)/2 + i
+    double uvec[NQ];     // active multipliers during a rebuild
+    int ivec[NQ];        // active constraint ids during a rebuild
+    double dvec[NQ];
+    double ucon[64];
+    double w[NQ];
+};
+
+struct Lds {
+    Prob prob;
+    union {
+        UpdScratch u;
+        QpScratch q;
+    };
+};
+
+enum CenOff { CEN_C = 0, CEN_CD = 3, CEN_R = 6, CEN_HB = 9, CEN_Y = 15, CEN_ZETA = 21, CEN_POSE = 27,
+              CEN_VC = 33 };
+
+// ---------------------------------------------------------------------------------------
+// wave helpers
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return threadIdx.x; }
+
+__device__ __forceinline__ void wsync() { __syncthreads(); }  // one wave per workgroup
+
+__device__ __forceinline__ double bcast(double v, int lane) {
+    int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+    int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ int bcast_i(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+// argmin with deterministic tie-break on the index; result uniform in every lane
+__device__ __forceinline__ void wave_argmin(double& v, int& i) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        double ov = __shfl_xor(v, o);
+        int oi = __shfl_xor(i, o);
+        if (ov < v || (ov == v && oi < i)) { v = ov; i = oi; }
+    }
+}
+__device__ __forceinline__ bool wave_any(bool p) { return __any(p); }
+
+// ---------------------------------------------------------------------------------------
+// small fp64 linear algebra (row-major 3x3)
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void cross3(const double* a, const double* b, double* o) {
+    double x = a[1] * b[2] - a[2] * b[1];
+    double y = a[2] * b[0] - a[0] * b[2];
+    double z = a[0] * b[1] - a[1] * b[0];
+    o[0] = x; o[1] = y; o[2] = z;
+}
+__device__ __forceinline__ double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+__device__ __forceinline__ void mv3(const double* M, const double* v, double* o) {
+    double x = M[0] * v[0] + M[1] * v[1] + M[2] * v[2];
+    double y = M[3] * v[0] + M[4] * v[1] + M[5] * v[2];
+    double z = M[6] * v[0] + M[7] * v[1] + M[8] * v[2];
+    o[0] = x; o[1] = y; o[2] = z;
+}
+__device__ __forceinline__ void mm3(const double* A, const double* B, double* C) {
+    double t[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) t[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) C[k] = t[k];
+}
+// R I R^T
+__device__ __forceinline__ void rot_inertia(const double* R, const double* I, double* o) {
+    double t[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) t[3 * i + j] = R[3 * i] * I[j] + R[3 * i + 1] * I[3 + j] + R[3 * i + 2] * I[6 + j];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) o[3 * i + j] = t[3 * i] * R[3 * j] + t[3 * i + 1] * R[3 * j + 1] + t[3 * i + 2] * R[3 * j + 2];
+}
+__device__ __forceinline__ void inv3(const double* A, double* o) {
+    double c00 = A[4] * A[8] - A[5] * A[7], c01 = A[5] * A[6] - A[3] * A[8], c02 = A[3] * A[7] - A[4] * A[6];
+    double det = A[0] * c00 + A[1] * c01 + A[2] * c02;
+    double id = 1.0 / det;
+    o[0] = c00 * id; o[1] = (A[2] * A[7] - A[1] * A[8]) * id; o[2] = (A[1] * A[5] - A[2] * A[4]) * id;
+    o[3] = c01 * id; o[4] = (A[0] * A[8] - A[2] * A[6]) * id; o[5] = (A[2] * A[3] - A[0] * A[5]) * id;
+    o[6] = c02 * id; o[7] = (A[1] * A[6] - A[0] * A[7]) * id; o[8] = (A[0] * A[4] - A[1] * A[3]) * id;
+}
+// rotation by angle q about unit axis a (Rodrigues)
+__device__ __forceinline__ void axis_rot(const double* a, double q, double* R) {
+    double s, c;
+    sincos(q, &s, &c);
+    double v = 1.0 - c;
+    R[0] = c + a[0] * a[0] * v;        R[1] = a[0] * a[1] * v - a[2] * s; R[2] = a[0] * a[2] * v + a[1] * s;
+    R[3] = a[1] * a[0] * v + a[2] * s; R[4] = c + a[1] * a[1] * v;        R[5] = a[1] * a[2] * v - a[0] * s;
+    R[6] = a[2] * a[0] * v - a[1] * s; R[7] = a[2] * a[1] * v + a[0] * s; R[8] = c + a[2] * a[2] * v;
+}
+// Eigen::Quaterniond(w,x,y,z).toRotationMatrix() (cpp:209-213)
+__device__ __forceinline__ void quat_R(double qx, double qy, double qz, double qw, double* R) {
+    double tx = 2 * qx, ty = 2 * qy, tz = 2 * qz;
+    double twx = tx * qw, twy = ty * qw, twz = tz * qw;
+    double txx = tx * qx, txy = ty * qx, txz = tz * qx;
+    double tyy = ty * qy, tyz = tz * qy, tzz = tz * qz;
+    R[0] = 1 - (tyy + tzz); R[1] = txy - twz;       R[2] = txz + twy;
+    R[3] = txy + twz;       R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
+}
+__device__ __forceinline__ int rp(int i, int j) { return j * (j + 1) / 2 + i; }  // packed upper (i <= j)
+
+// ---------------------------------------------------------------------------------------
+// update phase
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ double sel3(const double* v, int k) { return k == 0 ? v[0] : (k == 1 ? v[1] : v[2]); }
+
+// ---------------------------------------------------------------------------------------
+// update phase (≙ updateState, cpp:256-294, plus the per-cycle terms of solveQP that do not
+// depend on the QP: computeDesiredWrench cpp:426-445, swing commands cpp:447-464, bounds cpp:503-515)
+// ---------------------------------------------------------------------------------------
+__device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
+    UpdScratch& s = L.u;
+    Prob& P = L.prob;
+    const wbc_model& md = *a.model;
+    const wbc_params& pr = *a.params;
+    const int lane = lane_id();
+    const int kap = a.contacts[rb];
+    const bool switching = a.switching[rb] != 0;
+    const bool stateful = a.stateful != 0;
+    const bool debug = a.debug != 0;
+    double* H = stateful ? a.hist + (size_t)rb * HIST_LEN : nullptr;
+
+    // U1: inputs, one element per lane (robot-major arrays -> contiguous per wave)
+    {
+        bool bad = false;
+        for (int k = lane; k < 91; k += 64) {
+            double v;
+            if (k < 7) v = a.base_pose[(size_t)rb * 7 + k];
+            else if (k < 25) v = a.nu[(size_t)rb * 18 + (k - 7)];
+            else if (k < 37) v = a.qj[(size_t)rb * 12 + (k - 25)];
+            else v = a.ref[(size_t)rb * 54 + (k - 37)];
+            bad |= !isfinite(v);
+            s.in[k] = v;
+        }
+        bool anybad = wave_any(bad);
+        if (lane == 0) { P.flags = anybad ? 1.0 : 0.0; P.kappa = (double)kap; }
+    }
+    wsync();
+    const double* pB = &s.in[0];
+    const double* vB = &s.in[7];
+    const double* wB = &s.in[10];
+    const double* qd = &s.in[13];
+    const double* qj = &s.in[25];
+    const double* ref = &s.in[37];
+    double RB[9];
+    quat_R(s.in[3], s.in[4], s.in[5], s.in[6], RB);
+
+    // U3: forward kinematics + velocity / bias-acceleration recursion, one lane per body
+    if (lane < 12) {
+        const int l = lane / 3, kk = lane % 3;
+        double Rp[9], op[3], wp[3], alp[3] = {0, 0, 0}, aop[3] = {0, 0, 0}, vop[3];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) Rp[i] = RB[i];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) { op[i] = pB[i]; wp[i] = wB[i]; vop[i] = vB[i]; }
+        double aj[3] = {0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            if (k <= kk) {
+                const wbc_link& lk = md.link[l][k];
+                double Rj[9], oj[3], Rl[9], rel[3], t[3];
+                mm3(Rp, lk.R, Rj);
+                mv3(Rp, lk.p, oj);
+                oj[0] += op[0]; oj[1] += op[1]; oj[2] += op[2];
+                mv3(Rj, lk.axis, aj);
+                axis_rot(lk.axis, qj[3 * l + k], Rl);
+                mm3(Rj, Rl, Rp);  // child body orientation
+                const double qdk = qd[3 * l + k];
+                rel[0] = oj[0] - op[0]; rel[1] = oj[1] - op[1]; rel[2] = oj[2] - op[2];
+                double vo[3], ao[3], u[3];
+                cross3(wp, rel, t);
+                vo[0] = vop[0] + t[0]; vo[1] = vop[1] + t[1]; vo[2] = vop[2] + t[2];
+                cross3(alp, rel, ao);
+                cross3(wp, t, u);
+                ao[0] += aop[0] + u[0]; ao[1] += aop[1] + u[1]; ao[2] += aop[2] + u[2];
+                cross3(wp, aj, t);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    alp[i] = alp[i] + t[i] * qdk;
+                    wp[i] = wp[i] + aj[i] * qdk;
+                    op[i] = oj[i]; aop[i] = ao[i]; vop[i] = vo[i];
+                }
+            }
+        }
+        const wbc_link& lk = md.link[l][kk];
+        const int b = 1 + lane;
+        double c[3], I[9], rel[3], t[3], u[3];
+        mv3(Rp, lk.com, c);
+        c[0] += op[0]; c[1] += op[1]; c[2] += op[2];
+        rot_inertia(Rp, lk.inertia, I);
+        rel[0] = c[0] - op[0]; rel[1] = c[1] - op[1]; rel[2] = c[2] - op[2];
+        double vc[3], ac[3];
+        cross3(wp, rel, t);
+        vc[0] = vop[0] + t[0]; vc[1] = vop[1] + t[1]; vc[2] = vop[2] + t[2];
+        cross3(alp, rel, ac);
+        cross3(wp, t, u);
+        ac[0] += aop[0] + u[0]; ac[1] += aop[1] + u[1]; ac[2] += aop[2] + u[2];
+        double Iw[3], Ia[3], wIw[3];
+        mv3(I, wp, Iw);
+        mv3(I, alp, Ia);
+        cross3(wp, Iw, wIw);
+        const double m = lk.mass;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            s.bc[b][i] = c[i];
+            s.bw[b][i] = wp[i];
+            s.bv[b][i] = vc[i];
+            s.bF[b][i] = m * ac[i];
+            s.bN[b][i] = Ia[i] + wIw[i];
+            s.ja[lane][i] = aj[i];
+            s.jo[lane][i] = op[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 9; ++i) s.bI[b][i] = I[i];
+        s.bm[b] = m;
+        if (kk == 2) {
+            double pf[3], rf[3], vf[3];
+            mv3(Rp, md.foot[l], pf);
+            pf[0] += op[0]; pf[1] += op[1]; pf[2] += op[2];
+            rf[0] = pf[0] - op[0]; rf[1] = pf[1] - op[1]; rf[2] = pf[2] - op[2];
+            cross3(wp, rf, t);
+            vf[0] = vop[0] + t[0]; vf[1] = vop[1] + t[1]; vf[2] = vop[2] + t[2];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) { s.pf[l][i] = pf[i]; s.vf[l][i] = vf[i]; }
+        }
+    } else if (lane == 12) {
+        double c[3], I[9], rel[3], t[3], u[3], Iw[3], wIw[3];
+        mv3(RB, md.base_com, c);
+        c[0] += pB[0]; c[1] += pB[1]; c[2] += pB[2];
+        rot_inertia(RB, md.base_inertia, I);
+        rel[0] = c[0] - pB[0]; rel[1] = c[1] - pB[1]; rel[2] = c[2] - pB[2];
+        cross3(wB, rel, t);
+        cross3(wB, t, u);
+        mv3(I, wB, Iw);
+        cross3(wB, Iw, wIw);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            s.bc[0][i] = c[i];
+            s.bw[0][i] = wB[i];
+            s.bv[0][i] = vB[i] + t[i];
+            s.bF[0][i] = md.base_mass * u[i];
+            s.bN[0][i] = wIw[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 9; ++i) s.bI[0][i] = I[i];
+        s.bm[0] = md.base_mass;
+    }
+    wsync();
+    // foot Jacobian joint columns (getFrameFreeFloatingJacobian rows 0-2, cpp:327-341): a_k x (p_f - o_k)
+    if (lane < 12) {
+        const int l = lane / 3, k = lane % 3;
+        double dd[3] = {s.pf[l][0] - s.jo[lane][0], s.pf[l][1] - s.jo[lane][1], s.pf[l][2] - s.jo[lane][2]}, col[3];
+        cross3(s.ja[lane], dd, col);
+#pragma unroll
+        for (int r = 0; r < 3; ++r) s.Jf[l][3 * r + k] = col[r];
+    }
+
+    // U4: CoM and its velocity (cpp:260-261), centroidal inertia I_c
+    double c[3] = {0, 0, 0}, cd[3] = {0, 0, 0}, m = 0.0;
+    for (int b = 0; b < 13; ++b) {
+        const double mb = s.bm[b];
+        m += mb;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) { c[i] += mb * s.bc[b][i]; cd[i] += mb * s.bv[b][i]; }
+    }
+    const double inv_m = 1.0 / m;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { c[i] *= inv_m; cd[i] *= inv_m; }
+    const double r[3] = {c[0] - pB[0], c[1] - pB[1], c[2] - pB[2]};
+    if (lane < 13) {
+        const int b = lane;
+        const double mb = s.bm[b];
+        double d[3] = {s.bc[b][0] - c[0], s.bc[b][1] - c[1], s.bc[b][2] - c[2]};
+        const double dd = dot3(d, d);
+        const double* I = s.bI[b];
+        s.contrib[b][0] = I[0] + mb * (dd - d[0] * d[0]);
+        s.contrib[b][1] = I[4] + mb * (dd - d[1] * d[1]);
+        s.contrib[b][2] = I[8] + mb * (dd - d[2] * d[2]);
+        s.contrib[b][3] = I[1] - mb * d[0] * d[1];
+        s.contrib[b][4] = I[2] - mb * d[0] * d[2];
+        s.contrib[b][5] = I[5] - mb * d[1] * d[2];
+    }
+    wsync();
+    double Ic[9], Icinv[9];
+    {
+        double t[6] = {0, 0, 0, 0, 0, 0};
+        for (int b = 0; b < 13; ++b)
+#pragma unroll
+            for (int k = 0; k < 6; ++k) t[k] += s.contrib[b][k];
+        Ic[0] = t[0]; Ic[4] = t[1]; Ic[8] = t[2];
+        Ic[1] = Ic[3] = t[3]; Ic[2] = Ic[6] = t[4]; Ic[5] = Ic[7] = t[5];
+        inv3(Ic, Icinv);
+    }
+    wsync();
+    if (lane < 13) {  // base bias: sum F ; sum (c_b - p_B) x F + N
+        const int b = lane;
+        double rb_[3] = {s.bc[b][0] - pB[0], s.bc[b][1] - pB[1], s.bc[b][2] - pB[2]}, t[3];
+        cross3(rb_, s.bF[b], t);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) { s.contrib[b][i] = s.bF[b][i]; s.contrib[b][3 + i] = t[i] + s.bN[b][i]; }
+    }
+    // U5: per joint: centroidal momentum column (about c), leg block of M, joint bias (C nu)_j
+    if (lane < 12) {
+        const int j = lane, l = j / 3, k = j % 3;
+        const double aj[3] = {s.ja[j][0], s.ja[j][1], s.ja[j][2]};
+        const double oj[3] = {s.jo[j][0], s.jo[j][1], s.jo[j][2]};
+        double Al[3] = {0, 0, 0}, Aa[3] = {0, 0, 0}, hsum[3] = {0, 0, 0}, Mrow[3] = {0, 0, 0};
+#pragma unroll
+        for (int kk = 0; kk < 3; ++kk) {
+            if (kk >= k) {
+                const int b = 1 + 3 * l + kk;
+                const double mb = s.bm[b];
+                const double cb[3] = {s.bc[b][0], s.bc[b][1], s.bc[b][2]};
+                double rel[3] = {cb[0] - oj[0], cb[1] - oj[1], cb[2] - oj[2]}, v[3], t[3], Ia[3], fm[3];
+                cross3(aj, rel, v);
+                double dc[3] = {cb[0] - c[0], cb[1] - c[1], cb[2] - c[2]};
+                cross3(dc, v, t);
+                mv3(s.bI[b], aj, Ia);
+                cross3(rel, s.bF[b], fm);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    Al[i] += mb * v[i];
+                    Aa[i] += mb * t[i] + Ia[i];
+                    hsum[i] += fm[i] + s.bN[b][i];
+                }
+#pragma unroll
+                for (int k2 = 0; k2 < 3; ++k2) {
+                    if (kk >= k2) {
+                        const int j2 = 3 * l + k2;
+                        const double a2[3] = {s.ja[j2][0], s.ja[j2][1], s.ja[j2][2]};
+                        double rel2[3] = {cb[0] - s.jo[j2][0], cb[1] - s.jo[j2][1], cb[2] - s.jo[j2][2]}, v2[3], Ia2[3];
+                        cross3(a2, rel2, v2);
+                        mv3(s.bI[b], a2, Ia2);
+                        Mrow[k2] += mb * dot3(v, v2) + dot3(aj, Ia2);
+                    }
+                }
+            }
+        }
+        double KA[3];
+        mv3(Icinv, Aa, KA);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            s.A[j][i] = Al[i]; s.A[j][3 + i] = Aa[i]; s.Mjj[j][i] = Mrow[i]; s.KA[j][i] = KA[i];
+        }
+        s.hj[j] = dot3(aj, hsum);
+    }
+    wsync();
+    double hb[6] = {0, 0, 0, 0, 0, 0};
+    for (int b = 0; b < 13; ++b)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) hb[k] += s.contrib[b][k];
+
+    // y = Tdot_inv(previous cycle) nu  (quirk A.3: nu, not T nu; one-cycle lag)
+    double y[6] = {0, 0, 0, 0, 0, 0};
+    bool hvalid = false;
+    int kap_old = 15;
+    if (stateful) {
+        hvalid = H[H_VALID] != 0.0;
+        kap_old = (int)H[H_KOLD];
+        if (hvalid) {
+            double yl = 0.0;
+            if (lane < 6) {
+                for (int cc = 0; cc < 18; ++cc) yl += H[H_TDINV + lane * 18 + cc] * s.in[7 + cc];
+            }
+#pragma unroll
+            for (int k = 0; k < 6; ++k) y[k] = bcast(yl, k);
+        }
+    }
+    // h' = C nu + M[:, 0:6] y ; M_bb = [[m I, -m S(r)], [m S(r), I_c - m S(r)^2]]
+    double hp[6], zeta[6];
+    {
+        double t[3], u[3], w[3], Icy[3];
+        cross3(r, &y[3], t);
+        cross3(r, t, u);
+        mv3(Ic, &y[3], Icy);
+        cross3(r, y, w);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            hp[i] = hb[i] + m * (y[i] - t[i]);
+            hp[3 + i] = hb[3 + i] + m * w[i] + Icy[i] - m * u[i];
+        }
+        double hca[3];
+        cross3(r, hp, t);
+        hca[0] = hp[3] - t[0]; hca[1] = hp[4] - t[1]; hca[2] = hp[5] - t[2];
+        zeta[0] = hp[0] * inv_m; zeta[1] = hp[1] * inv_m; zeta[2] = hp[2] * inv_m;
+        mv3(Icinv, hca, &zeta[3]);  // zeta = Mbar_b^-1 Ad^T h'_b
+    }
+    if (lane == 0) {
+        double* cen = s.cen;
+        cen[CEN_C] = c[0]; cen[CEN_C + 1] = c[1]; cen[CEN_C + 2] = c[2];
+        cen[CEN_CD] = cd[0]; cen[CEN_CD + 1] = cd[1]; cen[CEN_CD + 2] = cd[2];
+        cen[CEN_R] = r[0]; cen[CEN_R + 1] = r[1]; cen[CEN_R + 2] = r[2];
+        // currentPose_ = [c; eulAnglesRPY(R)] (cpp:262-264), centerOfMassVelocity_ = [c_dot; omega_B] (cpp:261)
+        cen[CEN_POSE] = c[0]; cen[CEN_POSE + 1] = c[1]; cen[CEN_POSE + 2] = c[2];
+        cen[CEN_POSE + 3] = atan2(RB[7], RB[8]);
+        cen[CEN_POSE + 4] = atan2(-RB[6], sqrt(RB[7] * RB[7] + RB[8] * RB[8]));
+        cen[CEN_POSE + 5] = atan2(RB[3], RB[0]);
+        cen[CEN_VC] = cd[0]; cen[CEN_VC + 1] = cd[1]; cen[CEN_VC + 2] = cd[2];
+        cen[CEN_VC + 3] = wB[0]; cen[CEN_VC + 4] = wB[1]; cen[CEN_VC + 5] = wB[2];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) cen[CEN_HB + i] = hp[i];
+        P.m = m; P.inv_m = inv_m;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) { P.Ic[i] = Ic[i]; P.Icinv[i] = Icinv[i]; }
+    }
+    const double dt = 1.0 / pr.loop_rate;
+
+    // U6/U7/U8: lane = joint column j: Jbar joint column, Mbar_j column, bbar_j
+    if (lane < 12) {
+        const int j = lane, lj = j / 3, kj = j % 3;
+        const double Alj[3] = {s.A[j][0], s.A[j][1], s.A[j][2]}, Aaj[3] = {s.A[j][3], s.A[j][4], s.A[j][5]};
+        const double KAj[3] = {s.KA[j][0], s.KA[j][1], s.KA[j][2]};
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+            double d[3] = {s.pf[l][0] - c[0], s.pf[l][1] - c[1], s.pf[l][2] - c[2]}, t[3];
+            cross3(d, KAj, t);
+#pragma unroll
+            for (int rr = 0; rr < 3; ++rr) {
+                const double jf = (l == lj) ? s.Jf[l][3 * rr + kj] : 0.0;
+                P.Jbj[(3 * l + rr) * 12 + j] = jf - Alj[rr] * inv_m + t[rr];
+            }
+        }
+        for (int i = 0; i < 12; ++i) {
+            double Mij = (i / 3 == lj) ? s.Mjj[j][i % 3] : 0.0;
+            Mij -= (s.A[i][0] * Alj[0] + s.A[i][1] * Alj[1] + s.A[i][2] * Alj[2]) * inv_m;
+            Mij -= s.A[i][3] * KAj[0] + s.A[i][4] * KAj[1] + s.A[i][5] * KAj[2];
+            P.Mbj[i * 12 + j] = Mij;
+        }
+        double t[3];
+        cross3(r, Alj, t);
+        const double hpj = s.hj[j] + dot3(Alj, y) + (t[0] + Aaj[0]) * y[3] + (t[1] + Aaj[1]) * y[4] + (t[2] + Aaj[2]) * y[5];
+        P.bbj[j] = hpj - (dot3(Alj, zeta) + dot3(Aaj, &zeta[3]));
+        P.d[j] = s.pf[lj][kj] - sel3(c, kj);
+    }
+    // U9: T_top = [Ad^-1(r), Mbar_b^-1 A_j]; Tdot_inv for the next cycle (cpp:291-293)
+    double tcol[6] = {0, 0, 0, 0, 0, 0};
+    if (stateful) {
+        double dr[3] = {0, 0, 0};
+        if (!switching) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) dr[i] = (r[i] - H[H_ROLD + i]) / dt;
+        }
+        if (lane >= 3 && lane < 6) {  // lin rows, cols 3..5: S(dr)
+            const int cc = lane - 3;
+            double e[3] = {cc == 0 ? 1.0 : 0.0, cc == 1 ? 1.0 : 0.0, cc == 2 ? 1.0 : 0.0};
+            cross3(dr, e, tcol);
+        } else if (lane >= 6 && lane < 18) {
+            const int j = lane - 6;
+            double Tj[6];
+#pragma unroll
+            for (int rr = 0; rr < 3; ++rr) {
+                Tj[rr] = switching ? 0.0 : (s.A[j][rr] * inv_m - H[H_MAOLD + rr * 12 + j]) / dt;
+                Tj[3 + rr] = switching ? 0.0 : (s.KA[j][rr] - H[H_MAOLD + (3 + rr) * 12 + j]) / dt;
+            }
+            double t1[3], t2[3];
+            cross3(dr, s.KA[j], t1);
+            cross3(r, &Tj[3], t2);
+#pragma unroll
+            for (int rr = 0; rr < 3; ++rr) {
+                tcol[rr] = -(t1[rr] + Tj[rr] + t2[rr]);
+                tcol[3 + rr] = -Tj[3 + rr];
+            }
+        }
+    }
+    wsync();  // all reads of the old history and of U6 outputs done
+    if (stateful) {
+        if (lane < 18) {
+#pragma unroll
+            for (int rr = 0; rr < 6; ++rr) H[H_TDINV + rr * 18 + lane] = tcol[rr];
+        }
+        if (lane < 12) {
+            const int j = lane;
+#pragma unroll
+            for (int rr = 0; rr < 3; ++rr) {
+                H[H_MAOLD + rr * 12 + j] = s.A[j][rr] * inv_m;
+                H[H_MAOLD + (3 + rr) * 12 + j] = s.KA[j][rr];
+            }
+        }
+    }
+    // U10: finite-difference bounds (cpp:384-402, 503-515); swing commands (cpp:447-464)
+    if (lane < 12) {
+        const int i = lane, l = i / 3, rr = i % 3;
+        const double d[3] = {P.d[3 * l], P.d[3 * l + 1], P.d[3 * l + 2]};
+        const double w3[3] = {s.cen[CEN_VC + 3], s.cen[CEN_VC + 4], s.cen[CEN_VC + 5]};
+        double wxd[3];
+        cross3(w3, d, wxd);
+        double cur = s.cen[CEN_VC + rr] + sel3(wxd, rr);
+        for (int j = 0; j < 12; ++j) cur += P.Jbj[i * 12 + j] * qd[j];
+        double old = 0.0;
+        if (stateful && hvalid) {
+            const double dol[3] = {H[H_DOLD + 3 * l], H[H_DOLD + 3 * l + 1], H[H_DOLD + 3 * l + 2]};
+            double wxo[3];
+            cross3(w3, dol, wxo);
+            old = s.cen[CEN_VC + rr] + sel3(wxo, rr);
+            for (int j = 0; j < 12; ++j) old += H[H_JBJOLD + i * 12 + j] * qd[j];
+        }
+        const double kn = (kap >> l) & 1, ko = (kap_old >> l) & 1;
+        double jc_dot = 0.0, js_dot = 0.0;
+        if (!switching) {
+            jc_dot = (kn * cur - ko * old) / dt;
+            js_dot = ((1.0 - kn) * cur - (1.0 - ko) * old) / dt;
+        }
+        const double cmd = (ref[42 + i] + pr.kd_swing * (ref[30 + i] - s.vf[l][rr]) + pr.kp_swing * (ref[18 + i] - s.pf[l][rr])) *
+                           (1.0 - kn);
+        P.r1[i] = -jc_dot;
+        P.rsw[i] = cmd - js_dot;
+    }
+    // U11: desired wrench (cpp:426-445); integralError_ update after use (cpp:442)
+    if (lane < 6) {
+        const int k = lane;
+        const double kp = (k == 2) ? pr.kp_z : pr.kp;
+        const double eint = (stateful && hvalid) ? H[H_EINT + k] : 0.0;
+        double mba;
+        if (k < 3) mba = m * ref[12 + k];
+        else mba = P.Ic[3 * (k - 3)] * ref[15] + P.Ic[3 * (k - 3) + 1] * ref[16] + P.Ic[3 * (k - 3) + 2] * ref[17];
+        const double e = s.cen[CEN_POSE + k] - ref[k];
+        const double Wk = -kp * e - pr.kd * (s.cen[CEN_VC + k] - ref[6 + k]) - pr.ki * eint + (k == 2 ? m * pr.gravity : 0.0) + mba;
+        P.W[k] = Wk;
+        if (stateful) H[H_EINT + k] = eint + e / pr.loop_rate;
+    }
+    wsync();
+    if (stateful) {
+        for (int k = lane; k < 144; k += 64) H[H_JBJOLD + k] = P.Jbj[k];
+        if (lane < 12) H[H_DOLD + lane] = P.d[lane];
+        if (lane < 3) H[H_ROLD + lane] = s.cen[CEN_R + lane];
+        if (lane == 0) { H[H_KOLD] = (double)kap; H[H_VALID] = 1.0; }
+    }
+    if (debug) {
+        double* D = a.dbg + (size_t)rb * WBC_DBG_LEN;
+        if (lane < 3) {
+            D[WBC_DBG_COM + lane] = s.cen[CEN_C + lane];
+            D[WBC_DBG_COMVEL + lane] = s.cen[CEN_CD + lane];
+        }
+        if (lane < 6) {
+            D[WBC_DBG_POSE + lane] = s.cen[CEN_POSE + lane];
+            D[WBC_DBG_VC + lane] = s.cen[CEN_VC + lane];
+            D[WBC_DBG_WRENCH + lane] = P.W[lane];
+            // bbar_b = Ad^T h'_b (not used by the controller)
+            const double* h6 = &s.cen[CEN_HB];
+            double t[3];
+            cross3(r, h6, t);
+            D[WBC_DBG_BBAR + lane] = (lane < 3) ? h6[lane] : h6[lane] - sel3(t, lane - 3);
+        }
+        for (int e = lane; e < 324; e += 64) {
+            const int i = e / 18, j = e % 18;
+            double v;
+            // S(r) entry (a, b)
+            auto Sr = [&](int aa, int bb) -> double {
+                if (aa == bb) return 0.0;
+                if (aa == 0) return bb == 1 ? -r[2] : r[1];
+                if (aa == 1) return bb == 0 ? r[2] : -r[0];
+                return bb == 0 ? -r[1] : r[0];
+            };
+            if (i < 6 && j < 6) {
+                if (i < 3 && j < 3) v = (i == j) ? m : 0.0;
+                else if (i < 3) v = -m * Sr(i, j - 3);
+                else if (j < 3) v = m * Sr(i - 3, j);
+                else {
+                    const int ii = i - 3, jj = j - 3;
+                    v = P.Ic[3 * ii + jj] - m * (Sr(ii, 0) * Sr(0, jj) + Sr(ii, 1) * Sr(1, jj) + Sr(ii, 2) * Sr(2, jj));
+                }
+            } else if (i < 6 || j < 6) {
+                const int bi = (i < 6) ? i : j, jj = (i < 6) ? j - 6 : i - 6;
+                if (bi < 3) v = s.A[jj][bi];
+                else {
+                    double t[3];
+                    cross3(r, s.A[jj], t);
+                    v = sel3(t, bi - 3) + s.A[jj][bi];
+                }
+            } else {
+                const int ji = i - 6, jj = j - 6;
+                v = (ji / 3 == jj / 3) ? s.Mjj[ji][jj % 3] : 0.0;
+            }
+            D[WBC_DBG_M + e] = v;
+        }
+        if (lane < 18) D[WBC_DBG_CNU + lane] = (lane < 6) ? sel3(lane < 3 ? hb : &hb[3], lane % 3) : s.hj[lane - 6];
+        for (int e = lane; e < 216; e += 64) {
+            const int i = e / 18, j = e % 18, l = i / 3, rr = i % 3;
+            double v, vb;
+            if (j < 3) {
+                v = vb = (rr == j) ? 1.0 : 0.0;
+            } else if (j < 6) {
+                // -S(p) e_(j-3) = e_(j-3) x p, row rr
+                const double pfB[3] = {s.pf[l][0] - pB[0], s.pf[l][1] - pB[1], s.pf[l][2] - pB[2]};
+                const double dl[3] = {P.d[3 * l], P.d[3 * l + 1], P.d[3 * l + 2]};
+                double e3[3] = {j == 3 ? 1.0 : 0.0, j == 4 ? 1.0 : 0.0, j == 5 ? 1.0 : 0.0}, t[3], t2[3];
+                cross3(e3, pfB, t);
+                cross3(e3, dl, t2);
+                v = sel3(t, rr);
+                vb = sel3(t2, rr);
+            } else {
+                v = ((j - 6) / 3 == l) ? s.Jf[l][3 * rr + (j - 6) % 3] : 0.0;
+                vb = P.Jbj[i * 12 + (j - 6)];
+            }
+            D[WBC_DBG_JFEET + e] = v;
+            D[WBC_DBG_JBAR + e] = vb;
+        }
+        if (lane < 12) {
+            D[WBC_DBG_PFEET + lane] = s.pf[lane / 3][lane % 3];
+            D[WBC_DBG_VFEET + lane] = s.vf[lane / 3][lane % 3];
+            D[WBC_DBG_R1 + lane] = P.r1[lane];
+            D[WBC_DBG_RSW + lane] = P.rsw[lane];
+            D[WBC_DBG_BBAR + 6 + lane] = P.bbj[lane];
+        }
+        if (lane < 36) {
+            const int i = lane / 6, j = lane % 6;
+            double v = 0.0;
+            if (i < 3 && j < 3) v = (i == j) ? m : 0.0;
+            else if (i >= 3 && j >= 3) v = P.Ic[3 * (i - 3) + (j - 3)];
+            D[WBC_DBG_MBARB + lane] = v;
+        }
+        for (int e = lane; e < 144; e += 64) D[WBC_DBG_MBARJ + e] = P.Mbj[e];
+    }
+    wsync();
+}
+
+// ---------------------------------------------------------------------------------------
+// solve phase: reduced QP (24 variables), Goldfarb-Idnani, one constraint per lane
+// ---------------------------------------------------------------------------------------
+struct QpMap {
+    int kap, ns, nsw, neq, nfr, ntq, m;
+};
+
+__device__ __forceinline__ QpMap make_map(int kap) {
+    QpMap q;
+    q.kap = kap;
+    q.ns = __builtin_popcount(kap & 15);
+    q.nsw = 4 - q.ns;
+    q.neq = 3 * q.ns;
+    q.nfr = 4 * q.ns;
+    q.ntq = 24;
+    q.m = q.neq + q.nfr + q.ntq + 6 * q.nsw;
+    return q;
+}
+// index of the idx-th leg whose contact bit equals `want`
+__device__ __forceinline__ int nth_leg(int kap, int idx, int want) {
+    int cnt = 0, leg = 0;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+        if ((((kap >> l) & 1) == want)) {
+            if (cnt == idx) leg = l;
+            ++cnt;
+        }
+    }
+    return leg;
+}
+
+// Normal n (24) and bound b of constraint p, as n^T y >= b (equalities: n^T y = b).
+// y = [qdd (12); slot l = f_l (stance) or s_l (swing), l = 0..3].
+__device__ void build_normal(const Prob& P, const QpMap& mp, const wbc_params& pr, int p, double* n, double& b,
+                             bool& is_eq) {
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) n[k] = 0.0;
+    b = 0.0;
+    is_eq = false;
+    if (p >= mp.m) return;
+    const double g0 = pr.gravity;
+    const int kap = mp.kap;
+    // adds  Jc_com[l,k] Mbar_b^-1 Jc_com[mm,:]^T  to the stance slots (coefficient of f_mm):
+    //   delta(k,rr)/m + (d_l x e_k) . I_c^-1 (d_mm x e_rr)
+    auto slot_coupling = [&](int l, int k) {
+        const double dl[3] = {P.d[3 * l], P.d[3 * l + 1], P.d[3 * l + 2]};
+        double e[3] = {k == 0 ? 1.0 : 0.0, k == 1 ? 1.0 : 0.0, k == 2 ? 1.0 : 0.0}, u[3], v[3];
+        cross3(dl, e, u);
+        mv3(P.Icinv, u, v);
+#pragma unroll
+        for (int mm = 0; mm < 4; ++mm) {
+            if ((kap >> mm) & 1) {
+                const double dm[3] = {P.d[3 * mm], P.d[3 * mm + 1], P.d[3 * mm + 2]};
+                // (d_mm x e_rr) . v = e_rr . (v x d_mm)
+                double vx[3];
+                cross3(v, dm, vx);
+#pragma unroll
+                for (int rr = 0; rr < 3; ++rr) n[12 + 3 * mm + rr] += ((k == rr) ? P.inv_m : 0.0) + vx[rr];
+            }
+        }
+    };
+    if (p < mp.neq) {  // R1, stance rows: Jc_j qdd + Jc_com a = r1 with a = Mbar_b^-1 (Jc^T f - gw)
+        const int l = nth_leg(kap, p / 3, 1), k = p % 3, i = 3 * l + k;
+        for (int j = 0; j < 12; ++j) n[j] = P.Jbj[i * 12 + j];
+        slot_coupling(l, k);
+        b = P.r1[i] + (k == 2 ? g0 : 0.0);
+        is_eq = true;
+    } else if (p < mp.neq + mp.nfr) {  // R2 friction pyramid (cpp:404-424): -D_rr f_l >= 0
+        const int q = p - mp.neq, l = nth_leg(kap, q / 4, 1), rr = q % 4;
+        const double nx = (rr == 0) ? -1.0 : (rr == 1 ? 1.0 : 0.0);
+        const double ny = (rr == 2) ? -1.0 : (rr == 3 ? 1.0 : 0.0);
+#pragma unroll
+        for (int ll = 0; ll < 4; ++ll) {
+            if (ll == l) {
+                n[12 + 3 * ll + 0] = nx;
+                n[12 + 3 * ll + 1] = ny;
+                n[12 + 3 * ll + 2] = pr.friction;
+            }
+        }
+    } else if (p < mp.neq + mp.nfr + mp.ntq) {  // R3 torque limits (cpp:495,506,513)
+        const int q = p - mp.neq - mp.nfr, i = q / 2;
+        const double sg = (q & 1) ? -1.0 : 1.0;
+        for (int j = 0; j < 12; ++j) n[j] = sg * P.Mbj[i * 12 + j];
+#pragma unroll
+        for (int mm = 0; mm < 4; ++mm) {
+            if ((kap >> mm) & 1) {
+#pragma unroll
+                for (int rr = 0; rr < 3; ++rr) n[12 + 3 * mm + rr] = -sg * P.Jbj[(3 * mm + rr) * 12 + i];
+            }
+        }
+        b = (sg > 0) ? (-pr.max_torque - P.bbj[i]) : (-pr.max_torque + P.bbj[i]);
+    } else {  // R4 / R5 swing rows (cpp:496-497,507-508,514-515)
+        const int q = p - mp.neq - mp.nfr - mp.ntq, l = nth_leg(kap, q / 6, 0), k = (q % 6) / 2, i = 3 * l + k;
+        const double sg = (q & 1) ? -1.0 : 1.0;  // +: w + s >= c' (R5) ; -: -w + s >= -c' (R4)
+        for (int j = 0; j < 12; ++j) n[j] = P.Jbj[i * 12 + j];
+        slot_coupling(l, k);
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) n[j] *= sg;
+#pragma unroll
+        for (int ll = 0; ll < 4; ++ll)
+#pragma unroll
+            for (int kk = 0; kk < 3; ++kk)
+                if (ll == l && kk == k) n[12 + 3 * ll + kk] = 1.0;
+        b = sg * (P.rsw[i] + (k == 2 ? g0 : 0.0));
+    }
+}
+
+// C0[:, p] = J0^T n_p with J0 = blkdiag(I12, L^-T); also the initial slack n^T x0 - b
+__device__ void init_column(const QpScratch& s, const double* n, double b, double* cc, double& sp, double& nrm) {
+    double nn = 0.0, sx = 0.0;
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) nn += n[k] * n[k];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        cc[k] = n[k];
+        sx += n[12 + k] * s.xs[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        double acc = 0.0;
+#pragma unroll
+        for (int i = 0; i <= k; ++i) acc += s.Linv[k][i] * n[12 + i];
+        cc[12 + k] = acc;
+    }
+    nrm = sqrt(fmax(nn, 1e-300));
+    sp = sx - b;
+}
+
+// Add the constraint whose column d is in s.dvec at position q: Householder on rows q..23 of every
+// lane's C column; R^-1 gains the column [-r / alpha; 1 / alpha] (rk = r of slot `lane`).
+__device__ __forceinline__ void add_column(QpScratch& s, int q, double zn, double rk, double* cc) {
+    const int lane = lane_id();
+    const double nrm2 = sqrt(zn);
+    const double dq = s.dvec[q];
+    const double alpha = (dq >= 0.0) ? -nrm2 : nrm2;
+    const double beta = 1.0 / (nrm2 * (nrm2 + fabs(dq)));
+    double vw = 0.0;
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+        double vk = (k >= q) ? s.dvec[k] : 0.0;
+        if (k == q) vk -= alpha;
+        vw += vk * cc[k];
+    }
+    vw *= beta;
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+        double vk = (k >= q) ? s.dvec[k] : 0.0;
+        if (k == q) vk -= alpha;
+        cc[k] -= vw * vk;
+    }
+    const double ia = 1.0 / alpha;
+    if (lane < q) s.Rinv[rp(lane, q)] = -rk * ia;
+    if (lane == q) s.Rinv[rp(q, q)] = ia;
+}
+
+__device__ __forceinline__ void load_d(QpScratch& s, int p, const double* cc) {
+    if (lane_id() == p) {
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) s.dvec[k] = cc[k];
+    }
+    wsync();
+}
+__device__ __forceinline__ double rinv_times_d(const QpScratch& s, int q) {
+    const int lane = lane_id();
+    double acc = 0.0;
+    if (lane < q)
+        for (int j = lane; j < q; ++j) acc += s.Rinv[rp(lane, j)] * s.dvec[j];
+    return acc;
+}
+
+__device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
+    const Prob& P = L.prob;
+    QpScratch& s = L.q;
+    const wbc_params& pr = *a.params;
+    const int lane = lane_id();
+    const int kap = (int)P.kappa;
+    const QpMap mp = make_map(kap);
+    int status = WBC_QP_OK;
+    int iters = 0;
+    const double inv_m = P.inv_m;
+
+    if (P.flags != 0.0) status = WBC_QP_NUMERIC;
+    {   // vacuous rows (quirk A.12): swing-leg rows of R1 read 0 = r1
+        bool bad = false;
+        if (lane < 12 && !((kap >> (lane / 3)) & 1)) bad = fabs(P.r1[lane]) > 1e-9 * fmax(1.0, fabs(P.r1[lane]));
+        if (wave_any(bad) && status == WBC_QP_OK) status = WBC_QP_INFEASIBLE;
+    }
+
+    // slot Hessian H_s = I + Jc_com (I + Mbar_b^-2) Jc_com^T on stance slots, slack_weight I on swing slots
+    if (lane < 12) {
+        const int i = lane, li = i / 3, ri = i % 3;
+        const bool sti = (kap >> li) & 1;
+        const double di[3] = {P.d[3 * li], P.d[3 * li + 1], P.d[3 * li + 2]};
+        double e[3] = {ri == 0 ? 1.0 : 0.0, ri == 1 ? 1.0 : 0.0, ri == 2 ? 1.0 : 0.0}, ui[3];
+        cross3(di, e, ui);
+        double t[3], t2[3], Gu[3];
+        mv3(P.Icinv, ui, t);
+        mv3(P.Icinv, t, t2);
+        Gu[0] = ui[0] + t2[0]; Gu[1] = ui[1] + t2[1]; Gu[2] = ui[2] + t2[2];
+        for (int j = 0; j < 12; ++j) {
+            const int lj = j / 3, rj = j % 3;
+            const bool stj = (kap >> lj) & 1;
+            double h = 0.0;
+            if (sti && stj) {
+                const double dj[3] = {P.d[3 * lj], P.d[3 * lj + 1], P.d[3 * lj + 2]};
+                double ej[3] = {rj == 0 ? 1.0 : 0.0, rj == 1 ? 1.0 : 0.0, rj == 2 ? 1.0 : 0.0}, uj[3];
+                cross3(dj, ej, uj);
+                h = (i == j ? 1.0 : 0.0) + (ri == rj ? 1.0 + inv_m * inv_m : 0.0) + dot3(Gu, uj);
+            } else if (!sti && i == j) {
+                h = pr.slack_weight;
+            }
+            s.Hs[i][j] = h;
+        }
+        // g_s = -Jc_com (W + [0, 0, g/m, 0, 0, 0])
+        s.gs[i] = sti ? -(P.W[ri] + (ri == 2 ? pr.gravity * inv_m : 0.0) + dot3(ui, &P.W[3])) : 0.0;
+    }
+    wsync();
+    bool chol_ok = true;
+    for (int k = 0; k < 12; ++k) {  // H_s = L L^T, lane i owns row i
+        const double dkk = s.Hs[k][k];
+        if (!(dkk > 0.0)) chol_ok = false;
+        const double lkk = sqrt(fmax(dkk, 1e-300));
+        if (lane > k && lane < 12) s.Hs[lane][k] *= 1.0 / lkk;
+        wsync();
+        if (lane > k && lane < 12) {
+            const double lik = s.Hs[lane][k];
+            for (int j = k + 1; j <= lane; ++j) s.Hs[lane][j] -= lik * s.Hs[j][k];
+        }
+        if (lane == k) s.Hs[k][k] = lkk;
+        wsync();
+    }
+    if (!chol_ok && status == WBC_QP_OK) status = WBC_QP_NUMERIC;
+    if (lane < 12) {  // Linv = L^-1, lane j solves L x = e_j
+        const int j = lane;
+        for (int i = 0; i < 12; ++i) {
+            double acc = (i == j) ? 1.0 : 0.0;
+            for (int k = j; k < i; ++k) acc -= s.Hs[i][k] * s.Linv[k][j];
+            s.Linv[i][j] = (i < j) ? 0.0 : acc / s.Hs[i][i];
+        }
+    }
+    wsync();
+    if (lane < 12) {  // x0 = -H^-1 g, slot part: xs = -Linv^T (Linv g_s)
+        double acc = 0.0;
+        for (int i = 0; i <= lane; ++i) acc += s.Linv[lane][i] * s.gs[i];
+        s.tmp[lane] = acc;
+    }
+    wsync();
+    if (lane < 12) {
+        double acc = 0.0;
+        for (int k = lane; k < 12; ++k) acc += s.Linv[k][lane] * s.tmp[k];
+        s.xs[lane] = -acc;
+    }
+    wsync();
+
+    double cc[NQ];
+    double bp = 0.0, sp = 0.0, nrm = 1.0;
+    bool is_eq = false, active = false;
+    const bool is_con = lane < mp.m;
+    {
+        double n[NQ];
+        build_normal(P, mp, pr, lane, n, bp, is_eq);
+        init_column(s, n, bp, cc, sp, nrm);
+    }
+
+    // Goldfarb-Idnani (wave-uniform control flow)
+    int q = 0;         // active set size
+    double u = 0.0;    // multiplier of active slot `lane`
+    int act = -1;      // constraint id of active slot `lane`
+    int neq_added = 0; // equalities occupy slots 0..neq_added-1
+    int next_eq = 0;
+    int pstar = -1;
+    double up = 0.0;
+    const double tiny = 1e-26;
+    bool done = (status != WBC_QP_OK);
+
+    while (!done) {
+        bool eq_step = false;
+        if (pstar < 0) {
+            if (next_eq < mp.neq) {
+                pstar = next_eq++;
+                eq_step = true;
+            } else {
+                double v = 1e300;
+                if (is_con && !is_eq && !active) {
+                    const double tol = 1e-10 * fmax(1.0, fabs(bp));
+                    if (sp < -tol) v = sp / nrm;
+                }
+                int idx = lane;
+                wave_argmin(v, idx);
+                if (!(v < 1e299)) break;  // no violated constraint: optimal
+                pstar = idx;
+            }
+            up = 0.0;
+        }
+        if (!eq_step) {
+            if (++iters > pr.max_wsr) { status = WBC_QP_MAX_ITER; iters = pr.max_wsr; break; }
+        }
+        load_d(s, pstar, cc);
+        const double rk = rinv_times_d(s, q);
+        double zn = 0.0, cz = 0.0;
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) {
+            const double dk = (k >= q) ? s.dvec[k] : 0.0;
+            zn += dk * dk;
+            cz += cc[k] * dk;  // (C2^T d2)_p = n_p^T z
+        }
+        const double sps = bcast(sp, pstar);
+        if (eq_step && zn <= tiny * fmax(1.0, bcast(nrm, pstar) * bcast(nrm, pstar))) {
+            if (fabs(sps) <= 1e-9 * fmax(1.0, fabs(bcast(bp, pstar)))) {  // redundant, consistent
+                pstar = -1;
+                continue;
+            }
+            status = WBC_QP_INFEASIBLE;
+            break;
+        }
+        double t1 = 1e300;
+        int l1 = 64;
+        if (!eq_step) {  // partial step: keep active inequality multipliers >= 0
+            double v = 1e300;
+            if (lane < q && lane >= neq_added && rk > 1e-14) v = u / rk;
+            l1 = lane;
+            wave_argmin(v, l1);
+            t1 = v;
+        }
+        const double t2 = (zn > tiny) ? (-sps / zn) : 1e300;
+        const double t = eq_step ? t2 : fmin(t1, t2);
+        if (!(t < 1e299)) { status = WBC_QP_INFEASIBLE; break; }
+        const bool full = eq_step || (t2 < 1e299 && t2 <= t1);
+        if (t2 < 1e299) sp += t * cz;
+        if (lane < q) u -= t * rk;
+        up += t;
+        if (full) {
+            add_column(s, q, zn, rk, cc);
+            if (lane == q) { u = up; act = pstar; }
+            if (lane == pstar) active = true;
+            ++q;
+            if (eq_step) neq_added = q;
+            pstar = -1;
+            wsync();
+        } else {
+            // drop active slot l1: shift the active list, rebuild C and R^-1 by re-adding the rest
+            const int l = l1;
+            const int dropped = bcast_i(act, l);
+            if (lane == dropped) active = false;
+            {
+                const double un = __shfl(u, (lane + 1) & 63);
+                const int an = __shfl(act, (lane + 1) & 63);
+                if (lane >= l && lane < q - 1) { u = un; act = an; }
+                if (lane == q - 1) { u = 0.0; act = -1; }
+            }
+            --q;
+            double n[NQ], bb, spd, nd;
+            bool eqd;
+            build_normal(P, mp, pr, lane, n, bb, eqd);
+            init_column(s, n, bb, cc, spd, nd);  // fresh C0; slacks sp are kept
+            for (int k = 0; k < q; ++k) {
+                const int pk = bcast_i(act, k);
+                load_d(s, pk, cc);
+                const double rkk = rinv_times_d(s, k);
+                double znk = 0.0;
+#pragma unroll
+                for (int j = 0; j < NQ; ++j) {
+                    const double dj = (j >= k) ? s.dvec[j] : 0.0;
+                    znk += dj * dj;
+                }
+                add_column(s, k, znk, rkk, cc);
+                wsync();
+            }
+            // keep pstar (its slack was advanced); loop re-evaluates the step for it
+        }
+    }
+
+    // primal recovery: y = x0 + H^-1 sum_k u_k n_{a_k}
+    if (lane < 64) s.ucon[lane] = 0.0;
+    wsync();
+    if (lane < q && act >= 0) s.ucon[act] = u;
+    wsync();
+    double w[NQ];
+    {
+        double n[NQ], bb;
+        bool eqf;
+        build_normal(P, mp, pr, lane, n, bb, eqf);
+        const double uc = is_con ? s.ucon[lane] : 0.0;
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) w[k] = wave_sum(uc * n[k]);
+    }
+    if (lane < 12) {
+        double acc = 0.0;
+#pragma unroll
+        for (int i = 0; i < 12; ++i)
+            if (i <= lane) acc += s.Linv[lane][i] * w[12 + i];
+        s.tmp[lane] = acc;
+    }
+    wsync();
+    if (lane < 12) {
+        double acc = 0.0;
+        for (int k = lane; k < 12; ++k) acc += s.Linv[k][lane] * s.tmp[k];
+        s.dvec[12 + lane] = s.xs[lane] + acc;  // slot part of y
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 12; ++k) s.dvec[k] = w[k];  // qdd part of y
+    }
+    wsync();
+
+    // outputs: x (42, cpp:534-541), grf = x[18:30] (cpp:556-563), tau (cpp:565-576)
+    const bool ok = (status == WBC_QP_OK);
+    if (lane < 42) {
+        double xv;
+        if (lane < 6) {  // a = Mbar_b^-1 (Jc_com^T f - gw)
+            double F[3] = {0, 0, 0}, Mm[3] = {0, 0, 0};
+#pragma unroll
+            for (int l = 0; l < 4; ++l) {
+                if ((kap >> l) & 1) {
+                    const double fl[3] = {s.dvec[12 + 3 * l], s.dvec[13 + 3 * l], s.dvec[14 + 3 * l]};
+                    const double dl[3] = {P.d[3 * l], P.d[3 * l + 1], P.d[3 * l + 2]};
+                    double t[3];
+                    cross3(dl, fl, t);
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) { F[i] += fl[i]; Mm[i] += t[i]; }
+                }
+            }
+            if (lane < 3) xv = sel3(F, lane) * inv_m - (lane == 2 ? pr.gravity : 0.0);
+            else {
+                const int rr = lane - 3;
+                xv = P.Icinv[3 * rr] * Mm[0] + P.Icinv[3 * rr + 1] * Mm[1] + P.Icinv[3 * rr + 2] * Mm[2];
+            }
+        } else if (lane < 18) {
+            xv = s.dvec[lane - 6];
+        } else if (lane < 30) {
+            const int i = lane - 18;
+            xv = ((kap >> (i / 3)) & 1) ? s.dvec[12 + i] : 0.0;
+        } else {
+            const int i = lane - 30;
+            xv = ((kap >> (i / 3)) & 1) ? fabs(P.rsw[i]) : s.dvec[12 + i];
+        }
+        if (a.x) a.x[(size_t)rb * WBC_NV + lane] = ok ? xv : 0.0;
+    }
+    if (lane < 12) {
+        double tv = P.bbj[lane];
+        for (int i = 0; i < 12; ++i) {
+            const double fi = ((kap >> (i / 3)) & 1) ? s.dvec[12 + i] : 0.0;
+            tv += P.Mbj[lane * 12 + i] * s.dvec[i] - P.Jbj[i * 12 + lane] * fi;
+        }
+        const double fl = ((kap >> (lane / 3)) & 1) ? s.dvec[12 + lane] : 0.0;
+        a.tau[(size_t)rb * 12 + lane] = ok ? tv : 0.0;
+        a.grf[(size_t)rb * 12 + lane] = ok ? fl : 0.0;
+    }
+    if (lane == 0) {
+        a.status[rb] = status;
+        a.iters[rb] = iters;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// kernels
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64, WBC_WAVES_PER_SIMD) void wbc_step_kernel(KernelArgs a) {
+    __shared__ Lds L;
+    const int rb = blockIdx.x;
+    if (rb >= a.batch) return;
+    update_phase(a, rb, L);
+    solve_phase(a, rb, L);
+}
+
+__global__ __launch_bounds__(64, WBC_WAVES_PER_SIMD) void wbc_update_kernel(KernelArgs a) {
+    __shared__ Lds L;
+    const int rb = blockIdx.x;
+    if (rb >= a.batch) return;
+    update_phase(a, rb, L);
+    const double* src = reinterpret_cast<const double*>(&L.prob);
+    double* dst = a.work + (size_t)rb * PROB_LEN;
+    for (int k = lane_id(); k < PROB_LEN; k += 64) dst[k] = src[k];
+}
+
+__global__ __launch_bounds__(64, WBC_WAVES_PER_SIMD) void wbc_solve_kernel(KernelArgs a) {
+    __shared__ Lds L;
+    const int rb = blockIdx.x;
+    if (rb >= a.batch) return;
+    double* dst = reinterpret_cast<double*>(&L.prob);
+    const double* src = a.work + (size_t)rb * PROB_LEN;
+    for (int k = lane_id(); k < PROB_LEN; k += 64) dst[k] = src[k];
+    wsync();
+    solve_phase(a, rb, L);
+}
+
+__global__ void wbc_reset_kernel(double* hist, const uint8_t* mask, int batch) {
+    const int rb = blockIdx.x;
+    if (rb >= batch) return;
+    if (mask && !mask[rb]) return;
+    double* H = hist + (size_t)rb * HIST_LEN;
+    for (int k = threadIdx.x; k < HIST_LEN; k += blockDim.x) H[k] = (k == H_KOLD) ? 15.0 : 0.0;
+}
+
+}  // namespace wbc
+
+// Launchers used by the engine (wbc_engine.cpp); grid = one 64-lane workgroup per robot.
+extern "C" hipError_t wbc_launch_step(const wbc::KernelArgs* a, hipStream_t st) {
+    hipLaunchKernelGGL(wbc::wbc_step_kernel, dim3(a->batch), dim3(64), 0, st, *a);
+    return hipGetLastError();
+}
+extern "C" hipError_t wbc_launch_update(const wbc::KernelArgs* a, hipStream_t st) {
+    hipLaunchKernelGGL(wbc::wbc_update_kernel, dim3(a->batch), dim3(64), 0, st, *a);
+    return hipGetLastError();
+}
+extern "C" hipError_t wbc_launch_solve(const wbc::KernelArgs* a, hipStream_t st) {
+    hipLaunchKernelGGL(wbc::wbc_solve_kernel, dim3(a->batch), dim3(64), 0, st, *a);
+    return hipGetLastError();
+}
+extern "C" hipError_t wbc_launch_reset(double* hist, const uint8_t* mask, int batch, hipStream_t st) {
+    hipLaunchKernelGGL(wbc::wbc_reset_kernel, dim3(batch), dim3(64), 0, st, hist, mask, batch);
+    return hipGetLastError();
+}

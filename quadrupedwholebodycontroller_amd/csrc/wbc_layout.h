@@ -1,0 +1,70 @@
+// wbc_layout.h — device-side record layouts shared by the HIP kernel and the host engine.
+#ifndef WBC_LAYOUT_H
+#define WBC_LAYOUT_H
+
+#include "wbc.h"
+
+namespace wbc {
+
+// Per-robot history that survives between control cycles (stateful mode).  Compact form of
+// the reference's finite-difference state (hpp:154-161): T_old (top rows only vary:
+// [Ad^-1(r_old), Mbar_b^-1 A_j]), Jbar_old (com part [I, -S(p_f - c)] from d_old, joint part),
+// Tdot_inv (top 6 rows), integralError_, the contacts of Jbar_old, and a valid flag
+// (0 right after setInitialState: T_old = I, J_old = 0, Tdot_inv = 0, cpp:84-104).
+enum HistOff {
+    H_ROLD = 0,     // r_old = c - p_B of the previous cycle (3)
+    H_MAOLD = 3,    // Mbar_b^-1 A_j of the previous cycle, 6x12 row-major (72)
+    H_DOLD = 75,    // p_f - c, previous cycle (12)
+    H_JBJOLD = 87,  // joint part of Jbar_feet, previous cycle, 12x12 (144)
+    H_TDINV = 231,  // Tdot_inv top 6 rows, 6x18 row-major (108)
+    H_EINT = 339,   // integralError_ (6)
+    H_KOLD = 345,   // contact bitmask of the previous cycle (as double)
+    H_VALID = 346,  // 0 after reset
+    HIST_LEN = 348
+};
+
+// Assembled per-robot problem: written by the update phase, read by the solve phase
+// (the HBM workspace between wbc_update and wbc_solve; kept in LDS by the fused step).
+struct Prob {
+    double m, inv_m;
+    double Ic[9];
+    double Icinv[9];
+    double d[12];     // foot position minus CoM, LH, LF, RF, RH
+    double Jbj[144];  // joint columns of Jbar_feet = J_feet T^-1, [row 0..11][joint 0..11]
+    double Mbj[144];  // centroidMassMatrixJoints_
+    double bbj[12];   // centroidGeneralizedBias_(6:18)
+    double r1[12];    // R1 bound: -Jc_dot_com v_c - Jc_dot_j qdot (cpp:504)
+    double rsw[12];   // R4/R5 bound: cmd - Js_dot_com v_c - Js_dot_j qdot (cpp:507,515)
+    double W[6];      // computeDesiredWrench (cpp:426-445)
+    double kappa;     // contact bitmask
+    double flags;     // bit 0: non-finite input / intermediate
+};
+static_assert(sizeof(Prob) % 16 == 0, "Prob must keep 16-byte alignment");
+constexpr int PROB_LEN = sizeof(Prob) / sizeof(double);
+
+// Kernel arguments (one struct, passed by value).
+struct KernelArgs {
+    const wbc_model* model;
+    const wbc_params* params;
+    const double* base_pose;
+    const double* nu;
+    const double* qj;
+    const double* ref;
+    const uint8_t* contacts;
+    const uint8_t* switching;
+    double* hist;       // [B][HIST_LEN]
+    double* work;       // [B][PROB_LEN] (split update/solve)
+    double* tau;
+    double* grf;
+    double* x;
+    int32_t* status;
+    int32_t* iters;
+    double* dbg;        // [B][WBC_DBG_LEN]
+    int32_t batch;
+    int32_t stateful;   // read / write history
+    int32_t debug;      // write debug records
+};
+
+
+}  // namespace wbc
+#endif

@@ -1,0 +1,96 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the numpy oracle of the reference path.
+
+Tolerances (BASELINE.md parity gate; fp64 everywhere):
+  intermediates (M, C nu, Jacobians, CoM, Mbar, Jbar, bbar, wrench, bounds): 1e-10 relative to
+    max(1, |value|) -- the kernel uses closed forms instead of the reference's dense LU inverses,
+    so agreement is to rounding, not bitwise;
+  x*  within 1e-8 * (1 + |x*|_inf);   tau within 1e-7 N m * (1 + |tau|_inf) / 100;
+  QP status identical.
+"""
+import numpy as np
+import pytest
+
+import wbc_np as W
+from quadrupedwholebodycontroller_amd import DEBUG, STATELESS, Engine, split_debug, workloads
+
+pytestmark = pytest.mark.gpu
+
+MODEL = W.Model()
+PARAMS = W.default_params()
+
+
+def oracle_batch(inp, idx):
+    out = []
+    for b in idx:
+        c = W.ReferenceWBC(MODEL, PARAMS)
+        c.set_state(inp["base_pose"][b], inp["nu"][b], inp["qj"][b])
+        kap = [(int(inp["contacts"][b]) >> i) & 1 for i in range(4)]
+        c.set_reference(inp["ref"][b], kap, bool(inp["switching"][b]))
+        c.step()
+        out.append(c)
+    return out
+
+
+def run_engine(inp, flags=STATELESS | DEBUG):
+    B = inp["base_pose"].shape[0]
+    e = Engine(B)
+    e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
+    e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
+    e.step(flags)
+    out = e.outputs()
+    out["dbg"] = e.debug()
+    e.close()
+    return out
+
+
+def rel_err(a, b):
+    return np.max(np.abs(np.asarray(a) - np.asarray(b)) / np.maximum(1.0, np.abs(np.asarray(b))))
+
+
+def check_robot(ctrl, out, b, tol_int=1e-10):
+    d = split_debug(out["dbg"][b])
+    ref = ctrl.debug_record()
+    for k in ("com", "comvel", "pose", "vc", "M", "Cnu", "Jfeet", "pfeet", "vfeet", "Mbar_b", "Mbar_j", "Jbar",
+              "W", "r1", "rsw"):
+        assert rel_err(d[k], ref[k]) < tol_int, (b, k, rel_err(d[k], ref[k]))
+    assert rel_err(d["bbar"][6:], ref["bbar"][6:]) < tol_int, (b, "bbar")
+    assert out["status"][b] == ctrl.qp_status, (b, out["status"][b], ctrl.qp_status)
+    if ctrl.qp_status == W.QP_OK:
+        x = ctrl.qp_solution
+        assert np.max(np.abs(out["x"][b] - x)) <= 1e-8 * (1 + np.max(np.abs(x))), (b, "x")
+        assert np.max(np.abs(out["tau"][b] - ctrl.tau)) <= 1e-7 * (1 + np.max(np.abs(ctrl.tau))), (b, "tau")
+        assert np.max(np.abs(out["grf"][b] - ctrl.grf)) <= 1e-8 * (1 + np.max(np.abs(ctrl.grf))), (b, "grf")
+
+
+def test_stance_cold_parity():
+    inp = workloads.stance_cold(256, seed=11)
+    out = run_engine(inp)
+    ctrls = oracle_batch(inp, range(256))
+    for b, c in enumerate(ctrls):
+        check_robot(c, out, b)
+
+
+def test_random_modes_parity():
+    inp = workloads.rl_random(256, seed=12)
+    out = run_engine(inp)
+    ctrls = oracle_batch(inp, range(256))
+    for b, c in enumerate(ctrls):
+        check_robot(c, out, b)
+    # the mix must exercise swing legs, active inequalities and infeasible cases
+    assert len(set(int(k) for k in inp["contacts"])) == 16
+
+
+def test_update_solve_split_equals_fused():
+    inp = workloads.rl_random(512, seed=13)
+    B = 512
+    e = Engine(B)
+    e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
+    e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
+    e.step(STATELESS)
+    fused = e.outputs()
+    e.update(STATELESS)
+    e.solve(STATELESS)
+    split = e.outputs()
+    e.close()
+    for k in ("tau", "grf", "x", "status", "iters"):
+        assert np.array_equal(fused[k], split[k]), k

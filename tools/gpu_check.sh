@@ -1,0 +1,25 @@
+#!/bin/bash
+# One GPU-box session: each GPU step under its own timeout; stop at the first crash / timeout.
+# Exit codes 0 (pass) and 1 (Python test/assert failure) continue; anything else ends the script.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+TAG=${TAG:-run}
+step() {
+  local name=$1 t=$2; shift 2
+  echo "== $name (timeout $t s) $(date +%T)" >> gpurun_out/steps.log
+  timeout -k 10 "$t" "$@" > "gpurun_out/$TAG.$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc $(date +%T)" >> gpurun_out/steps.log
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name rc=$rc"; exit $rc; fi
+  return 0
+}
+for s in ${STEPS:-smoke pytest bench prof}; do
+  case $s in
+    smoke)  step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    pytest) step pytest 600 python -m pytest tests -m gpu -x -q ;;
+    bench)  step bench 400 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 ${BENCH_ARGS:-} ;;
+    prof)   step prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o $TAG --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
+  esac
+done
+echo done
