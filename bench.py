@@ -89,6 +89,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--extra", action="store_true", help="also time the other configs (reported under 'extra')")
+    ap.add_argument("--breakdown", action="store_true", help="also time the update and solve kernels separately")
     args = ap.parse_args()
 
     import torch
@@ -112,7 +113,10 @@ def main():
     gen = getattr(workloads, cfg["gen"])
     inp = gen(B, seed=cfg["seed"] + 1000 * rank)
 
-    stream = torch.cuda.current_stream()
+    # a dedicated (non-null) stream: the engine launches on it, the RCCL all-gather is ordered on it,
+    # and the HIP events below time it (the legacy null stream would be handle 0 = "engine default")
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     e = Engine(B, device=local_rank)
     e.set_stream(stream.cuda_stream)
     e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
@@ -159,6 +163,23 @@ def main():
     flops = float(np.sum(F_DYN + F_ASM + F_TAU + F_FACT + F_ITER * iters))
     achieved_tf = flops / (kernel_ms * 1e-3) / 1e12
     hbm_gbs = B * BYTES_COLD / (kernel_ms * 1e-3) / 1e9
+
+    breakdown = None
+    if args.breakdown:
+        ev0.record(stream)
+        for _ in range(args.steps):
+            e.update(STATELESS)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        upd_ms = ev0.elapsed_time(ev1) / args.steps
+        ev0.record(stream)
+        for _ in range(args.steps):
+            e.update(STATELESS)
+            e.solve(STATELESS)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        both_ms = ev0.elapsed_time(ev1) / args.steps
+        breakdown = dict(update_kernel_ms=upd_ms, solve_kernel_ms=both_ms - upd_ms, fused_kernel_ms=kernel_ms)
 
     extra = {}
     if args.extra and rank == 0:
@@ -215,6 +236,8 @@ def main():
     }
     if extra:
         result["extra"] = extra
+    if breakdown:
+        result["breakdown"] = breakdown
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(inp, args.cpu_budget)
         import multiprocessing

@@ -124,7 +124,8 @@ enum {
     WBC_DBG_WRENCH = 1014,  /* computeDesiredWrench (6)    cpp:426-445 */
     WBC_DBG_R1 = 1020,      /* R1 bounds: -Jc_dot v (12)   cpp:504 */
     WBC_DBG_RSW = 1032,     /* R4/R5 bound: cmd - Js_dot v (12) cpp:507,515 */
-    WBC_DBG_LEN = 1044
+    WBC_DBG_STAMPS = 1044,  /* diagnostic builds only (-DWBC_STAMPS): s_memtime per phase (8) */
+    WBC_DBG_LEN = 1052
 };
 
 typedef struct wbc_engine wbc_engine;

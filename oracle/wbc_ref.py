@@ -1,0 +1,151 @@
+"""ctypes wrapper of oracle/_build/libwbc_ref.so (the C restatement).  TEST INFRASTRUCTURE ONLY.
+
+Built by `make -C oracle` (also run by __graft_entry__.build()).  Used by tests/ as a fast
+checker and by bench.py as the CPU baseline.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB = os.path.join(HERE, "_build", "libwbc_ref.so")
+sys.path.insert(0, ROOT)
+
+_lib = None
+
+
+class KinDyn(C.Structure):
+    _fields_ = [("M", C.c_double * 324), ("Cnu", C.c_double * 18), ("foot_J", C.c_double * 216),
+                ("foot_pos", C.c_double * 12), ("foot_vel", C.c_double * 12), ("com", C.c_double * 3),
+                ("com_vel", C.c_double * 3), ("RB", C.c_double * 9)]
+
+
+class State(C.Structure):
+    _fields_ = [("old_T", C.c_double * 324), ("old_Jc", C.c_double * 216), ("old_Js", C.c_double * 216),
+                ("Tdot_inv", C.c_double * 324), ("e_int", C.c_double * 6), ("contacts", C.c_int),
+                ("first", C.c_int)]
+
+
+class Debug(C.Structure):
+    _fields_ = [("com", C.c_double * 3), ("comvel", C.c_double * 3), ("pose", C.c_double * 6),
+                ("vc", C.c_double * 6), ("M", C.c_double * 324), ("Cnu", C.c_double * 18),
+                ("Mbar_b", C.c_double * 36), ("Mbar_j", C.c_double * 144), ("Jbar", C.c_double * 216),
+                ("bbar", C.c_double * 18), ("W", C.c_double * 6), ("r1", C.c_double * 12), ("rsw", C.c_double * 12)]
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            raise OSError(f"{LIB} missing: run `make -C oracle`")
+        _lib = C.CDLL(LIB)
+        P = C.c_void_p
+        _lib.wbc_ref_kindyn.argtypes = [P, P, P, P, P]
+        _lib.wbc_ref_state_init.argtypes = [P]
+        _lib.wbc_ref_step.argtypes = [P, P, P, P, P, P, P, C.c_int, C.c_int, P, P, P, P, P]
+        _lib.wbc_ref_step.restype = C.c_int
+        _lib.wbc_ref_run_batch.argtypes = [P, P, C.c_int, P, P, P, P, P, P, P, P, P, P, P]
+    return _lib
+
+
+def _model_params():
+    from quadrupedwholebodycontroller_amd import _capi
+
+    m = _capi.WbcModel()
+    p = _capi.WbcParams()
+    # values come from the committed constants (no HIP device needed)
+    _fill_model(m)
+    _fill_params(p)
+    return m, p
+
+
+def _fill_params(p):
+    import wbc_np as W
+
+    d = W.default_params()
+    for k in ("friction", "loop_rate", "max_torque", "kp", "kp_z", "kd", "ki", "kp_swing", "kd_swing",
+              "slack_weight", "gravity"):
+        setattr(p, k, d[k])
+    for i, v in enumerate(d["initial_reference_pose"]):
+        p.initial_reference_pose[i] = v
+    p.max_wsr = d["max_wsr"]
+
+
+def _fill_model(m):
+    import wbc_np as W
+
+    md = W.Model()
+    m.base_mass = md.base_mass
+    for i in range(3):
+        m.base_com[i] = md.base_com[i]
+    for i in range(9):
+        m.base_inertia[i] = md.base_I.ravel()[i]
+    for l in range(4):
+        for k in range(3):
+            lk = m.link[l][k]
+            for i in range(9):
+                lk.R[i] = md.R[l, k].ravel()[i]
+                lk.inertia[i] = md.I[l, k].ravel()[i]
+            for i in range(3):
+                lk.p[i] = md.p[l, k, i]
+                lk.axis[i] = md.axis[l, k, i]
+                lk.com[i] = md.com[l, k, i]
+            lk.mass = md.mass[l, k]
+        for i in range(3):
+            m.foot[l][i] = md.foot[l, i]
+    m.total_mass = md.total_mass
+
+
+_MP = None
+
+
+def model_params():
+    global _MP
+    if _MP is None:
+        _MP = _model_params()
+    return _MP
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def run_batch(inp):
+    """Cold batch (every robot from setInitialState with the given switching flags)."""
+    m, p = model_params()
+    B = inp["base_pose"].shape[0]
+    f = lambda k, dt=np.float64: np.ascontiguousarray(inp[k], dt)
+    pose, nu, qj, ref = f("base_pose"), f("nu"), f("qj"), f("ref")
+    con, sw = f("contacts", np.uint8), f("switching", np.uint8)
+    out = dict(tau=np.zeros((B, 12)), grf=np.zeros((B, 12)), x=np.zeros((B, 42)), status=np.zeros(B, np.int32),
+               iters=np.zeros(B, np.int32))
+    lib().wbc_ref_run_batch(C.byref(m), C.byref(p), B, _p(pose), _p(nu), _p(qj), _p(ref), _p(con), _p(sw),
+                            _p(out["tau"]), _p(out["grf"]), _p(out["x"]), _p(out["status"]), _p(out["iters"]))
+    return out
+
+
+class Robot:
+    """Stateful single robot (the reference object across cycles)."""
+
+    def __init__(self):
+        self.st = State()
+        lib().wbc_ref_state_init(C.byref(self.st))
+
+    def step(self, pose, nu, qj, ref, contacts, switching, debug=False):
+        m, p = model_params()
+        tau, grf, x = np.zeros(12), np.zeros(12), np.zeros(42)
+        it = C.c_int()
+        dbg = Debug() if debug else None
+        a = [np.ascontiguousarray(v, np.float64) for v in (pose, nu, qj, ref)]
+        st = lib().wbc_ref_step(C.byref(m), C.byref(p), C.byref(self.st), *[_p(v) for v in a], int(contacts),
+                                int(switching), _p(tau), _p(grf), _p(x), C.byref(it),
+                                C.byref(dbg) if debug else None)
+        out = dict(tau=tau, grf=grf, x=x, status=st, iters=it.value)
+        if debug:
+            out["dbg"] = {k: np.array(getattr(dbg, k)) for k, _ in Debug._fields_}
+        return out

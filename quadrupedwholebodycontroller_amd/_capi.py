@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libwbc_hip.so")
+LIB_PATH = os.environ.get("WBC_LIB", os.path.join(HERE, "libwbc_hip.so"))
 
 NUM_JOINTS, NV, NC = 12, 42, 70
 POSE_LEN, NU_LEN, REF_LEN = 7, 18, 54
@@ -20,7 +20,7 @@ QP_OK, QP_MAX_ITER, QP_INFEASIBLE, QP_NUMERIC = 0, 1, 2, 3
 
 # WBC_DBG_* offsets (include/wbc.h)
 DBG = dict(COM=0, COMVEL=3, POSE=6, VC=12, M=18, CNU=342, JFEET=360, PFEET=576, VFEET=588, MBARB=600, MBARJ=636,
-           JBAR=780, BBAR=996, WRENCH=1014, R1=1020, RSW=1032, LEN=1044)
+           JBAR=780, BBAR=996, WRENCH=1014, R1=1020, RSW=1032, STAMPS=1044, LEN=1052)
 
 # every entry point declared in include/wbc.h
 C_API_SYMBOLS = [

@@ -178,6 +178,20 @@ __device__ __forceinline__ int rp(int i, int j) { return j * (j + 1) / 2 + i; } 
 // ---------------------------------------------------------------------------------------
 // update phase
 // ---------------------------------------------------------------------------------------
+// Diagnostic build only (-DWBC_STAMPS): lane 0 records the shader clock at phase boundaries into
+// the robot's debug record slots WBC_DBG_STAMPS.. (never read by the kernel, never an output).
+#ifdef WBC_STAMPS
+#define STAMP(a, rb, slot)                                                                             \
+    do {                                                                                               \
+        __builtin_amdgcn_sched_barrier(0);                                                             \
+        unsigned long long t_ = __builtin_amdgcn_s_memtime();                                          \
+        if (lane_id() == 0) (a).dbg[(size_t)(rb) * WBC_DBG_LEN + WBC_DBG_STAMPS + (slot)] = (double)t_; \
+        __builtin_amdgcn_sched_barrier(0);                                                             \
+    } while (0)
+#else
+#define STAMP(a, rb, slot) do { } while (0)
+#endif
+
 __device__ __forceinline__ double sel3(const double* v, int k) { return k == 0 ? v[0] : (k == 1 ? v[1] : v[2]); }
 
 // ---------------------------------------------------------------------------------------
@@ -944,6 +958,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
     }
     wsync();
 
+    STAMP(a, rb, 2);
     double cc[NQ];
     double bp = 0.0, sp = 0.0, nrm = 1.0;
     bool is_eq = false, active = false;
@@ -954,6 +969,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
         init_column(s, n, bp, cc, sp, nrm);
     }
 
+    STAMP(a, rb, 3);
     // Goldfarb-Idnani (wave-uniform control flow)
     int q = 0;         // active set size
     double u = 0.0;    // multiplier of active slot `lane`
@@ -1062,6 +1078,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
         }
     }
 
+    STAMP(a, rb, 4);
     // primal recovery: y = x0 + H^-1 sum_k u_k n_{a_k}
     if (lane < 64) s.ucon[lane] = 0.0;
     wsync();
@@ -1095,6 +1112,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
     }
     wsync();
 
+    STAMP(a, rb, 5);
     // outputs: x (42, cpp:534-541), grf = x[18:30] (cpp:556-563), tau (cpp:565-576)
     const bool ok = (status == WBC_QP_OK);
     if (lane < 42) {
@@ -1151,8 +1169,11 @@ __global__ __launch_bounds__(64, WBC_WAVES_PER_SIMD) void wbc_step_kernel(Kernel
     __shared__ Lds L;
     const int rb = blockIdx.x;
     if (rb >= a.batch) return;
+    STAMP(a, rb, 0);
     update_phase(a, rb, L);
+    STAMP(a, rb, 1);
     solve_phase(a, rb, L);
+    STAMP(a, rb, 6);
 }
 
 __global__ __launch_bounds__(64, WBC_WAVES_PER_SIMD) void wbc_update_kernel(KernelArgs a) {

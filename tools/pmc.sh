@@ -1,0 +1,18 @@
+#!/bin/bash
+# PMC passes for wbc_step_kernel (separate passes; never combined with trace domains).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${TAG:-pmc}
+OUT=gpurun_out/pmc_$TAG
+mkdir -p $OUT
+CMD="python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline"
+i=0
+for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" \
+           "SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU SQ_WAIT_INST_LDS" \
+           "FETCH_SIZE" "WRITE_SIZE" ${EXTRA_SETS:-}; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $set --kernel-trace --output-format csv -d $OUT -o pass$i -- $CMD > $OUT/pass$i.log 2>&1
+  rc=$?
+  echo "pass$i [$set] rc=$rc" >> $OUT/passes.txt
+  if [ $rc -ne 0 ]; then echo "pmc pass $i failed rc=$rc"; tail -5 $OUT/pass$i.log; if [ $rc -ne 1 ]; then exit $rc; fi; fi
+done
