@@ -1,0 +1,135 @@
+"""CPU-side checks of the boundary and of the multi-rank path.
+
+  * libwbc_hip.so loads and exports every entry point declared in include/wbc.h;
+  * the ctypes mirrors of wbc_model / wbc_params have the C layout (gcc sizeof/offsetof);
+  * without a GPU the product path fails loudly (no CPU fallback);
+  * world_size-2 gloo: each rank solves its shard (C restatement standing in for the HIP step on
+    CPU), the torque blocks are all-gathered, and the result equals the single-process batch.
+"""
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, "include", "wbc.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:int32_t|const char\*)\s+(wbc_\w+)\s*\(", txt, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    from quadrupedwholebodycontroller_amd import _capi
+
+    lib = _capi.load_library()
+    syms = header_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert sorted(_capi.C_API_SYMBOLS) == syms
+    out = subprocess.run(["nm", "-D", "--defined-only", _capi.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (wbc_\w+)", out))
+    assert set(syms) <= exported
+
+
+def test_struct_layout_matches_c():
+    import ctypes as C
+
+    from quadrupedwholebodycontroller_amd import _capi
+
+    src = r"""
+#include <stddef.h>
+#include <stdio.h>
+#include "wbc.h"
+int main(void){ printf("%zu %zu %zu %zu %zu %zu\n", sizeof(wbc_model), sizeof(wbc_params), sizeof(wbc_link),
+  offsetof(wbc_model, foot), offsetof(wbc_model, total_mass), offsetof(wbc_params, max_wsr)); return 0; }
+"""
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "s.c")
+        exe = os.path.join(d, "s")
+        open(c, "w").write(src)
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe], check=True)
+        vals = [int(v) for v in subprocess.run([exe], capture_output=True, text=True).stdout.split()]
+    assert vals == [C.sizeof(_capi.WbcModel), C.sizeof(_capi.WbcParams), C.sizeof(_capi.WbcLink),
+                    _capi.WbcModel.foot.offset, _capi.WbcModel.total_mass.offset, _capi.WbcParams.max_wsr.offset]
+
+
+def test_generated_model_header_matches_json():
+    """The C initializer (include/wbc_anymal_model.h) and the JSON hold the same constants."""
+    import ctypes as C
+
+    import wbc_ref
+
+    m, _ = wbc_ref.model_params()
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "m.c")
+        exe = os.path.join(d, "m")
+        open(c, "w").write('#include <stdio.h>\n#include "wbc_anymal_model.h"\nint main(void){ fwrite(&WBC_ANYMAL_MODEL, '
+                           'sizeof(wbc_model), 1, stdout); return 0; }\n')
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe], check=True)
+        raw = subprocess.run([exe], capture_output=True).stdout
+    assert raw == bytes(C.string_at(C.addressof(m), C.sizeof(m)))
+
+
+def test_no_silent_cpu_fallback():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from quadrupedwholebodycontroller_amd import Engine, WbcError
+
+    with pytest.raises(WbcError):
+        Engine(8)
+
+
+def test_shard_bounds():
+    from quadrupedwholebodycontroller_amd.sharding import shard_bounds
+
+    for total in (1, 7, 4096, 65536, 65537):
+        for world in (1, 2, 3, 8):
+            spans = [shard_bounds(total, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == total
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+            sizes = [h - l for l, h in spans]
+            assert max(sizes) - min(sizes) <= 1
+
+
+DIST_WORKER = r"""
+import os, sys
+import numpy as np
+import torch, torch.distributed as dist
+sys.path.insert(0, {root!r}); sys.path.insert(0, os.path.join({root!r}, "oracle"))
+from quadrupedwholebodycontroller_amd import workloads
+from quadrupedwholebodycontroller_amd.sharding import shard_bounds, all_gather_rows
+import wbc_ref
+dist.init_process_group("gloo")
+rank, world = dist.get_rank(), dist.get_world_size()
+B = 64
+inp = workloads.rl_random(B, seed=77)
+lo, hi = shard_bounds(B, world, rank)
+out = wbc_ref.run_batch({{k: v[lo:hi] for k, v in inp.items()}})
+tau = all_gather_rows(torch.from_numpy(out["tau"].ravel().copy()), world)
+st = all_gather_rows(torch.from_numpy(out["status"].astype(np.int64)), world)
+if rank == 0:
+    full = wbc_ref.run_batch(inp)
+    assert np.array_equal(tau.numpy().reshape(B, 12), full["tau"]), "gathered torques differ"
+    assert np.array_equal(st.numpy(), full["status"].astype(np.int64))
+    print("DIST_OK")
+dist.destroy_process_group()
+"""
+
+
+def test_two_rank_gloo_shard_and_gather(tmp_path):
+    script = tmp_path / "worker.py"
+    script.write_text(DIST_WORKER.format(root=ROOT))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=29531", str(script)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "DIST_OK" in r.stdout
