@@ -1,46 +1,55 @@
 // wbc_kernel.hip — batched whole-body-control step for gfx950 (MI355X), fp64.
 //
-// One robot per 64-lane wavefront (one workgroup = one wave).  Phases, each a device function
-// over the robot's LDS record:
+// One robot per 64-lane wavefront (one workgroup = one wave); 16 robots per CU (4 waves per
+// SIMD: <= 128 VGPRs, <= 10 KB of LDS per robot), so a 4096-robot batch is one pass of the chip.
 //
 //   update (≙ WholeBodyController::updateState, src/whole_body_controller.cpp:256-294)
-//     lanes 0..12 = rigid bodies: forward kinematics, body velocities, Newton-Euler bias terms
-//     (iDynTree KinDynComputations in MIXED representation, cpp:258-266,327-379,544-551);
-//     lanes 0..11 = joints: centroidal momentum matrix columns, leg blocks of M, joint bias;
-//     closed forms of T^-1, Mbar = T^-T M T^-1, Jbar = J T^-1, bbar (cpp:268-293) instead of the
-//     reference's seven dense 18x18 LU inverses; finite differences against the HBM history
-//     (computeDerivatives, cpp:384-402); desired wrench and swing commands (cpp:426-464).
+//     stage A  lanes 0..11 = joints: sin/cos; lanes 0..3 = legs: forward kinematics chain
+//              (3 links), joint-origin velocity and bias acceleration (iDynTree
+//              KinDynComputations in MIXED representation, cpp:258-266,327-379,544-551)
+//     stage B  lanes 0..12 = rigid bodies: com, world inertia, velocity, Newton-Euler bias force
+//     stage C  lanes 0..11 = joints: centroidal momentum matrix columns, leg blocks of M, joint bias;
+//              closed forms of T^-1, Mbar = T^-T M T^-1, Jbar = J T^-1, bbar (cpp:268-293) instead
+//              of the reference's seven dense 18x18 LU inverses; finite differences against the
+//              HBM history (cpp:384-402); desired wrench and swing commands (cpp:426-464).
 //   solve (≙ solveQP + computeJointTorques, cpp:466-577)
-//     The 42-variable / 70-row QP is reduced exactly to 24 variables and
-//     solved with the Goldfarb-Idnani dual active-set method: lane p owns constraint p and
-//     its column C[:,p] = J^T n_p (J = L^-T Q), so every product the method needs is lane-local;
-//     R^-1 (packed) lives in LDS; Householder reflections add constraints, Givens rotations drop
-//     them.  The primal solution is recovered from the final multipliers (x = x0 + H^-1 N u).
+//     The 42-variable / 70-row QP is reduced exactly to 24 variables and solved
+//     with the Goldfarb-Idnani dual active-set method: lane p owns constraint p and its column
+//     C[:,p] = J^T n_p (J = L^-T Q), so every product the method needs is lane-local; the chosen
+//     column is broadcast with v_readlane; R^-1 (packed) lives in LDS; Householder reflections
+//     add constraints; a drop re-adds the remaining active set.  The primal solution is recovered
+//     from the final multipliers (y = x0 + H^-1 N_A u) with an LDS transpose-sum.
 //
-// Nothing here is wave-size agnostic: 64-lane waves are assumed (gfx950).
+// 64-lane waves are assumed throughout (gfx950).
 #include <hip/hip_runtime.h>
 
 #include "wbc.h"
 #include "wbc_layout.h"
 
+#ifndef WBC_WAVES_PER_SIMD
+#define WBC_WAVES_PER_SIMD 4
+#endif
+
 namespace wbc {
 
-#ifndef WBC_WAVES_PER_SIMD
-#define WBC_WAVES_PER_SIMD 1
-#endif
-constexpr int NQ = 24;                 // reduced QP variables
+constexpr int NQ = 24;                  // reduced QP variables
 constexpr int RPACK = NQ * (NQ + 1) / 2;
 
+struct Frame {  // world frame of a body after stage A
+    double R[9], o[3], w[3], al[3], ao[3], vo[3];
+};
+struct Body {  // body quantities after stage B
+    double c[3], I[9], F[3], N[3], pad[6];
+};
+static_assert(sizeof(Frame) == sizeof(Body), "frame / body union");
 
 struct UpdScratch {
     double in[92];          // pose 7 | nu 18 | q 12 | ref 54
-    double bc[13][3];       // body com (world)
-    double bI[13][9];       // body inertia about com (world)
-    double bm[13];
-    double bw[13][3];       // body angular velocity
-    double bF[13][3];       // m * com acceleration at nu_dot = 0
-    double bN[13][3];       // I alpha + w x I w
-    double bv[13][3];       // com velocity
+    double sc[12][2];       // sin, cos of q_j
+    union {
+        Frame fr[13];
+        Body bd[13];
+    };
     double ja[12][3];       // joint axis (world)
     double jo[12][3];       // joint origin (world)
     double pf[4][3];
@@ -51,21 +60,17 @@ struct UpdScratch {
     double Mjj[12][3];      // leg block rows of M
     double hj[12];          // joint bias (C nu)_j
     double contrib[13][6];  // per-body partial sums
-    double cen[40];         // uniform scratch (see CEN_*)
+    double cen[40];         // uniform scratch (CEN_*)
 };
 
 struct QpScratch {
-    double Hs[12][13];   // slot Hessian, Cholesky in place (lower)
-    double Linv[12][13]; // L^-1
-    double gs[12];
-    double xs[12];       // slot part of x0 = -H^-1 g
-    double tmp[12];
-    double Rinv[RPACK];  // packed upper-triangular R^-1, column-major: (i,j) -> j(j+1)/2 + i
-    double uvec[NQ];     // active multipliers during a rebuild
-    int ivec[NQ];        // active constraint ids during a rebuild
-    double dvec[NQ];
+    double L[12][13];       // Cholesky factor of the slot Hessian (row-major, lower)
+    double xs[12];          // slot part of x0 = -H^-1 g
     double ucon[64];
-    double w[NQ];
+    union {
+        double Rinv[RPACK];  // packed upper-triangular R^-1, column-major: (i,j) -> j(j+1)/2 + i
+        double Wt[NQ][NQ];   // primal recovery: row k = u_k n_{a_k}
+    };
 };
 
 struct Lds {
@@ -76,14 +81,12 @@ struct Lds {
     };
 };
 
-enum CenOff { CEN_C = 0, CEN_CD = 3, CEN_R = 6, CEN_HB = 9, CEN_Y = 15, CEN_ZETA = 21, CEN_POSE = 27,
-              CEN_VC = 33 };
+enum CenOff { CEN_C = 0, CEN_CD = 3, CEN_R = 6, CEN_HB = 9, CEN_POSE = 27, CEN_VC = 33 };
 
 // ---------------------------------------------------------------------------------------
 // wave helpers
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ int lane_id() { return threadIdx.x; }
-
 __device__ __forceinline__ void wsync() { __syncthreads(); }  // one wave per workgroup
 
 __device__ __forceinline__ double bcast(double v, int lane) {
@@ -93,19 +96,40 @@ __device__ __forceinline__ double bcast(double v, int lane) {
 }
 __device__ __forceinline__ int bcast_i(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+    int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
 }
-// argmin with deterministic tie-break on the index; result uniform in every lane
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false); }
+
+template <int CTRL>
+__device__ __forceinline__ void argmin_step(double& v, int& i) {
+    const double ov = dpp_d<CTRL>(v);
+    const int oi = dpp_i<CTRL>(i);
+    const bool take = (ov < v) || (ov == v && oi < i);
+    v = take ? ov : v;
+    i = take ? oi : i;
+}
+// argmin over the wave, ties to the lowest index; result uniform.  DPP within 16-lane rows
+// (quad_perm, row_half_mirror, row_mirror), then the four row results via v_readlane.
 __device__ __forceinline__ void wave_argmin(double& v, int& i) {
+    argmin_step<0xB1>(v, i);   // quad_perm [1,0,3,2]
+    argmin_step<0x4E>(v, i);   // quad_perm [2,3,0,1]
+    argmin_step<0x141>(v, i);  // row_half_mirror
+    argmin_step<0x140>(v, i);  // row_mirror
+    double bv = bcast(v, 0);
+    int bi = bcast_i(i, 0);
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        double ov = __shfl_xor(v, o);
-        int oi = __shfl_xor(i, o);
-        if (ov < v || (ov == v && oi < i)) { v = ov; i = oi; }
+    for (int r = 16; r < 64; r += 16) {
+        const double ov = bcast(v, r);
+        const int oi = bcast_i(i, r);
+        if (ov < bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
     }
+    v = bv;
+    i = bi;
 }
 __device__ __forceinline__ bool wave_any(bool p) { return __any(p); }
 
@@ -134,8 +158,7 @@ __device__ __forceinline__ void mm3(const double* A, const double* B, double* C)
 #pragma unroll
     for (int k = 0; k < 9; ++k) C[k] = t[k];
 }
-// R I R^T
-__device__ __forceinline__ void rot_inertia(const double* R, const double* I, double* o) {
+__device__ __forceinline__ void rot_inertia(const double* R, const double* I, double* o) {  // R I R^T
     double t[9];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
@@ -148,17 +171,14 @@ __device__ __forceinline__ void rot_inertia(const double* R, const double* I, do
 }
 __device__ __forceinline__ void inv3(const double* A, double* o) {
     double c00 = A[4] * A[8] - A[5] * A[7], c01 = A[5] * A[6] - A[3] * A[8], c02 = A[3] * A[7] - A[4] * A[6];
-    double det = A[0] * c00 + A[1] * c01 + A[2] * c02;
-    double id = 1.0 / det;
+    double id = 1.0 / (A[0] * c00 + A[1] * c01 + A[2] * c02);
     o[0] = c00 * id; o[1] = (A[2] * A[7] - A[1] * A[8]) * id; o[2] = (A[1] * A[5] - A[2] * A[4]) * id;
     o[3] = c01 * id; o[4] = (A[0] * A[8] - A[2] * A[6]) * id; o[5] = (A[2] * A[3] - A[0] * A[5]) * id;
     o[6] = c02 * id; o[7] = (A[1] * A[6] - A[0] * A[7]) * id; o[8] = (A[0] * A[4] - A[1] * A[3]) * id;
 }
-// rotation by angle q about unit axis a (Rodrigues)
-__device__ __forceinline__ void axis_rot(const double* a, double q, double* R) {
-    double s, c;
-    sincos(q, &s, &c);
-    double v = 1.0 - c;
+// rotation about unit axis a by (s, c) = (sin q, cos q) (Rodrigues)
+__device__ __forceinline__ void axis_rot(const double* a, double s, double c, double* R) {
+    const double v = 1.0 - c;
     R[0] = c + a[0] * a[0] * v;        R[1] = a[0] * a[1] * v - a[2] * s; R[2] = a[0] * a[2] * v + a[1] * s;
     R[3] = a[1] * a[0] * v + a[2] * s; R[4] = c + a[1] * a[1] * v;        R[5] = a[1] * a[2] * v - a[0] * s;
     R[6] = a[2] * a[0] * v - a[1] * s; R[7] = a[2] * a[1] * v + a[0] * s; R[8] = c + a[2] * a[2] * v;
@@ -174,10 +194,8 @@ __device__ __forceinline__ void quat_R(double qx, double qy, double qz, double q
     R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
 }
 __device__ __forceinline__ int rp(int i, int j) { return j * (j + 1) / 2 + i; }  // packed upper (i <= j)
+__device__ __forceinline__ double sel3(const double* v, int k) { return k == 0 ? v[0] : (k == 1 ? v[1] : v[2]); }
 
-// ---------------------------------------------------------------------------------------
-// update phase
-// ---------------------------------------------------------------------------------------
 // Diagnostic build only (-DWBC_STAMPS): lane 0 records the shader clock at phase boundaries into
 // the robot's debug record slots WBC_DBG_STAMPS.. (never read by the kernel, never an output).
 #ifdef WBC_STAMPS
@@ -191,8 +209,6 @@ __device__ __forceinline__ int rp(int i, int j) { return j * (j + 1) / 2 + i; } 
 #else
 #define STAMP(a, rb, slot) do { } while (0)
 #endif
-
-__device__ __forceinline__ double sel3(const double* v, int k) { return k == 0 ? v[0] : (k == 1 ? v[1] : v[2]); }
 
 // ---------------------------------------------------------------------------------------
 // update phase (≙ updateState, cpp:256-294, plus the per-cycle terms of solveQP that do not
@@ -210,7 +226,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
     const bool debug = a.debug != 0;
     double* H = stateful ? a.hist + (size_t)rb * HIST_LEN : nullptr;
 
-    // U1: inputs, one element per lane (robot-major arrays -> contiguous per wave)
+    // inputs, one element per lane (robot-major arrays -> contiguous per wave); sin/cos per joint
     {
         bool bad = false;
         for (int k = lane; k < 91; k += 64) {
@@ -222,7 +238,13 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
             bad |= !isfinite(v);
             s.in[k] = v;
         }
-        bool anybad = wave_any(bad);
+        if (lane < 12) {
+            double sn, cs;
+            sincos(a.qj[(size_t)rb * 12 + lane], &sn, &cs);
+            s.sc[lane][0] = sn;
+            s.sc[lane][1] = cs;
+        }
+        const bool anybad = wave_any(bad);
         if (lane == 0) { P.flags = anybad ? 1.0 : 0.0; P.kappa = (double)kap; }
     }
     wsync();
@@ -230,110 +252,114 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
     const double* vB = &s.in[7];
     const double* wB = &s.in[10];
     const double* qd = &s.in[13];
-    const double* qj = &s.in[25];
     const double* ref = &s.in[37];
-    double RB[9];
-    quat_R(s.in[3], s.in[4], s.in[5], s.in[6], RB);
 
-    // U3: forward kinematics + velocity / bias-acceleration recursion, one lane per body
-    if (lane < 12) {
-        const int l = lane / 3, kk = lane % 3;
+    // stage A: one lane per leg walks HAA -> HFE -> KFE; lane 4 writes the base frame
+    if (lane < 4) {
+        const int l = lane;
         double Rp[9], op[3], wp[3], alp[3] = {0, 0, 0}, aop[3] = {0, 0, 0}, vop[3];
-#pragma unroll
-        for (int i = 0; i < 9; ++i) Rp[i] = RB[i];
+        quat_R(s.in[3], s.in[4], s.in[5], s.in[6], Rp);
 #pragma unroll
         for (int i = 0; i < 3; ++i) { op[i] = pB[i]; wp[i] = wB[i]; vop[i] = vB[i]; }
-        double aj[3] = {0, 0, 0};
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            if (k <= kk) {
-                const wbc_link& lk = md.link[l][k];
-                double Rj[9], oj[3], Rl[9], rel[3], t[3];
-                mm3(Rp, lk.R, Rj);
-                mv3(Rp, lk.p, oj);
-                oj[0] += op[0]; oj[1] += op[1]; oj[2] += op[2];
-                mv3(Rj, lk.axis, aj);
-                axis_rot(lk.axis, qj[3 * l + k], Rl);
-                mm3(Rj, Rl, Rp);  // child body orientation
-                const double qdk = qd[3 * l + k];
-                rel[0] = oj[0] - op[0]; rel[1] = oj[1] - op[1]; rel[2] = oj[2] - op[2];
-                double vo[3], ao[3], u[3];
-                cross3(wp, rel, t);
-                vo[0] = vop[0] + t[0]; vo[1] = vop[1] + t[1]; vo[2] = vop[2] + t[2];
-                cross3(alp, rel, ao);
-                cross3(wp, t, u);
-                ao[0] += aop[0] + u[0]; ao[1] += aop[1] + u[1]; ao[2] += aop[2] + u[2];
-                cross3(wp, aj, t);
+            const wbc_link& lk = md.link[l][k];
+            const int j = 3 * l + k;
+            double Rj[9], Rl[9], oj[3], aj[3], rel[3], t[3], u[3];
+            mm3(Rp, lk.R, Rj);
+            mv3(Rp, lk.p, oj);
+            oj[0] += op[0]; oj[1] += op[1]; oj[2] += op[2];
+            mv3(Rj, lk.axis, aj);
+            axis_rot(lk.axis, s.sc[j][0], s.sc[j][1], Rl);
+            mm3(Rj, Rl, Rp);  // child body orientation
+            const double qdk = qd[j];
+            rel[0] = oj[0] - op[0]; rel[1] = oj[1] - op[1]; rel[2] = oj[2] - op[2];
+            // the joint origin is a point of the parent: velocity / acceleration at nu_dot = 0
+            cross3(wp, rel, t);
+            cross3(wp, t, u);
+            double ao[3];
+            cross3(alp, rel, ao);
 #pragma unroll
-                for (int i = 0; i < 3; ++i) {
-                    alp[i] = alp[i] + t[i] * qdk;
-                    wp[i] = wp[i] + aj[i] * qdk;
-                    op[i] = oj[i]; aop[i] = ao[i]; vop[i] = vo[i];
-                }
+            for (int i = 0; i < 3; ++i) { vop[i] += t[i]; ao[i] += aop[i] + u[i]; }
+            cross3(wp, aj, t);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                alp[i] += t[i] * qdk;
+                wp[i] += aj[i] * qdk;
+                op[i] = oj[i];
+                aop[i] = ao[i];
+            }
+            Frame& f = s.fr[1 + j];
+#pragma unroll
+            for (int i = 0; i < 9; ++i) f.R[i] = Rp[i];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                f.o[i] = op[i]; f.w[i] = wp[i]; f.al[i] = alp[i]; f.ao[i] = aop[i]; f.vo[i] = vop[i];
+                s.ja[j][i] = aj[i]; s.jo[j][i] = op[i];
             }
         }
-        const wbc_link& lk = md.link[l][kk];
-        const int b = 1 + lane;
-        double c[3], I[9], rel[3], t[3], u[3];
-        mv3(Rp, lk.com, c);
-        c[0] += op[0]; c[1] += op[1]; c[2] += op[2];
-        rot_inertia(Rp, lk.inertia, I);
-        rel[0] = c[0] - op[0]; rel[1] = c[1] - op[1]; rel[2] = c[2] - op[2];
-        double vc[3], ac[3];
-        cross3(wp, rel, t);
-        vc[0] = vop[0] + t[0]; vc[1] = vop[1] + t[1]; vc[2] = vop[2] + t[2];
-        cross3(alp, rel, ac);
-        cross3(wp, t, u);
-        ac[0] += aop[0] + u[0]; ac[1] += aop[1] + u[1]; ac[2] += aop[2] + u[2];
-        double Iw[3], Ia[3], wIw[3];
-        mv3(I, wp, Iw);
-        mv3(I, alp, Ia);
-        cross3(wp, Iw, wIw);
-        const double m = lk.mass;
+    } else if (lane == 4) {
+        Frame& f = s.fr[0];
+        quat_R(s.in[3], s.in[4], s.in[5], s.in[6], f.R);
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            s.bc[b][i] = c[i];
-            s.bw[b][i] = wp[i];
-            s.bv[b][i] = vc[i];
-            s.bF[b][i] = m * ac[i];
-            s.bN[b][i] = Ia[i] + wIw[i];
-            s.ja[lane][i] = aj[i];
-            s.jo[lane][i] = op[i];
+        for (int i = 0; i < 3; ++i) { f.o[i] = pB[i]; f.w[i] = wB[i]; f.al[i] = 0.0; f.ao[i] = 0.0; f.vo[i] = vB[i]; }
+    }
+    wsync();
+
+    // stage B: one lane per body: com, world inertia, com velocity, m a_com, I alpha + w x I w
+    {
+        double c[3], I[9], vc[3], F[3], N[3], mb = 0.0;
+        if (lane < 13) {
+            const Frame& f = s.fr[lane];
+            const double* com;
+            const double* Il;
+            if (lane == 0) { mb = md.base_mass; com = md.base_com; Il = md.base_inertia; }
+            else {
+                const wbc_link& lk = md.link[(lane - 1) / 3][(lane - 1) % 3];
+                mb = lk.mass; com = lk.com; Il = lk.inertia;
+            }
+            double R[9], o[3], w[3], al[3], ao[3], vo[3], rel[3], t[3], u[3];
+#pragma unroll
+            for (int i = 0; i < 9; ++i) R[i] = f.R[i];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) { o[i] = f.o[i]; w[i] = f.w[i]; al[i] = f.al[i]; ao[i] = f.ao[i]; vo[i] = f.vo[i]; }
+            mv3(R, com, rel);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) c[i] = o[i] + rel[i];
+            rot_inertia(R, Il, I);
+            cross3(w, rel, t);
+            cross3(w, t, u);
+            double a3[3];
+            cross3(al, rel, a3);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) { vc[i] = vo[i] + t[i]; F[i] = mb * (ao[i] + a3[i] + u[i]); }
+            double Iw[3], Ia[3];
+            mv3(I, w, Iw);
+            mv3(I, al, Ia);
+            cross3(w, Iw, t);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) N[i] = Ia[i] + t[i];
+            if (lane >= 3 && (lane % 3) == 0) {  // SHANK bodies carry the foot frames (cpp:344-382)
+                const int l = lane / 3 - 1;
+                double pf[3], rf[3];
+                mv3(R, md.foot[l], rf);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) pf[i] = o[i] + rf[i];
+                cross3(w, rf, t);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) { s.pf[l][i] = pf[i]; s.vf[l][i] = vo[i] + t[i]; }
+            }
         }
+        wsync();  // every frame read before the union is overwritten
+        if (lane < 13) {
+            Body& bd = s.bd[lane];
 #pragma unroll
-        for (int i = 0; i < 9; ++i) s.bI[b][i] = I[i];
-        s.bm[b] = m;
-        if (kk == 2) {
-            double pf[3], rf[3], vf[3];
-            mv3(Rp, md.foot[l], pf);
-            pf[0] += op[0]; pf[1] += op[1]; pf[2] += op[2];
-            rf[0] = pf[0] - op[0]; rf[1] = pf[1] - op[1]; rf[2] = pf[2] - op[2];
-            cross3(wp, rf, t);
-            vf[0] = vop[0] + t[0]; vf[1] = vop[1] + t[1]; vf[2] = vop[2] + t[2];
+            for (int i = 0; i < 3; ++i) { bd.c[i] = c[i]; bd.F[i] = F[i]; bd.N[i] = N[i]; }
 #pragma unroll
-            for (int i = 0; i < 3; ++i) { s.pf[l][i] = pf[i]; s.vf[l][i] = vf[i]; }
+            for (int i = 0; i < 9; ++i) bd.I[i] = I[i];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) { s.contrib[lane][i] = mb * c[i]; s.contrib[lane][3 + i] = mb * vc[i]; }
         }
-    } else if (lane == 12) {
-        double c[3], I[9], rel[3], t[3], u[3], Iw[3], wIw[3];
-        mv3(RB, md.base_com, c);
-        c[0] += pB[0]; c[1] += pB[1]; c[2] += pB[2];
-        rot_inertia(RB, md.base_inertia, I);
-        rel[0] = c[0] - pB[0]; rel[1] = c[1] - pB[1]; rel[2] = c[2] - pB[2];
-        cross3(wB, rel, t);
-        cross3(wB, t, u);
-        mv3(I, wB, Iw);
-        cross3(wB, Iw, wIw);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            s.bc[0][i] = c[i];
-            s.bw[0][i] = wB[i];
-            s.bv[0][i] = vB[i] + t[i];
-            s.bF[0][i] = md.base_mass * u[i];
-            s.bN[0][i] = wIw[i];
-        }
-#pragma unroll
-        for (int i = 0; i < 9; ++i) s.bI[0][i] = I[i];
-        s.bm[0] = md.base_mass;
     }
     wsync();
     // foot Jacobian joint columns (getFrameFreeFloatingJacobian rows 0-2, cpp:327-341): a_k x (p_f - o_k)
@@ -344,36 +370,39 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
 #pragma unroll
         for (int r = 0; r < 3; ++r) s.Jf[l][3 * r + k] = col[r];
     }
-
-    // U4: CoM and its velocity (cpp:260-261), centroidal inertia I_c
-    double c[3] = {0, 0, 0}, cd[3] = {0, 0, 0}, m = 0.0;
-    for (int b = 0; b < 13; ++b) {
-        const double mb = s.bm[b];
-        m += mb;
+    // CoM and its velocity (getCenterOfMassPosition/Velocity, cpp:260-261)
+    double c[3] = {0, 0, 0}, cd[3] = {0, 0, 0};
+    double m = md.base_mass;
 #pragma unroll
-        for (int i = 0; i < 3; ++i) { c[i] += mb * s.bc[b][i]; cd[i] += mb * s.bv[b][i]; }
-    }
+    for (int l = 0; l < 4; ++l)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) m += md.link[l][k].mass;
+#pragma unroll 1
+    for (int b = 0; b < 13; ++b)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) { c[i] += s.contrib[b][i]; cd[i] += s.contrib[b][3 + i]; }
     const double inv_m = 1.0 / m;
 #pragma unroll
     for (int i = 0; i < 3; ++i) { c[i] *= inv_m; cd[i] *= inv_m; }
     const double r[3] = {c[0] - pB[0], c[1] - pB[1], c[2] - pB[2]};
-    if (lane < 13) {
-        const int b = lane;
-        const double mb = s.bm[b];
-        double d[3] = {s.bc[b][0] - c[0], s.bc[b][1] - c[1], s.bc[b][2] - c[2]};
+    wsync();  // contrib is reused
+    if (lane < 13) {  // centroidal inertia contributions
+        const double mb = (lane == 0) ? md.base_mass : md.link[(lane - 1) / 3][(lane - 1) % 3].mass;
+        const Body& bd = s.bd[lane];
+        double d[3] = {bd.c[0] - c[0], bd.c[1] - c[1], bd.c[2] - c[2]};
         const double dd = dot3(d, d);
-        const double* I = s.bI[b];
-        s.contrib[b][0] = I[0] + mb * (dd - d[0] * d[0]);
-        s.contrib[b][1] = I[4] + mb * (dd - d[1] * d[1]);
-        s.contrib[b][2] = I[8] + mb * (dd - d[2] * d[2]);
-        s.contrib[b][3] = I[1] - mb * d[0] * d[1];
-        s.contrib[b][4] = I[2] - mb * d[0] * d[2];
-        s.contrib[b][5] = I[5] - mb * d[1] * d[2];
+        s.contrib[lane][0] = bd.I[0] + mb * (dd - d[0] * d[0]);
+        s.contrib[lane][1] = bd.I[4] + mb * (dd - d[1] * d[1]);
+        s.contrib[lane][2] = bd.I[8] + mb * (dd - d[2] * d[2]);
+        s.contrib[lane][3] = bd.I[1] - mb * d[0] * d[1];
+        s.contrib[lane][4] = bd.I[2] - mb * d[0] * d[2];
+        s.contrib[lane][5] = bd.I[5] - mb * d[1] * d[2];
     }
     wsync();
     double Ic[9], Icinv[9];
     {
         double t[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll 1
         for (int b = 0; b < 13; ++b)
 #pragma unroll
             for (int k = 0; k < 6; ++k) t[k] += s.contrib[b][k];
@@ -383,13 +412,13 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
     }
     wsync();
     if (lane < 13) {  // base bias: sum F ; sum (c_b - p_B) x F + N
-        const int b = lane;
-        double rb_[3] = {s.bc[b][0] - pB[0], s.bc[b][1] - pB[1], s.bc[b][2] - pB[2]}, t[3];
-        cross3(rb_, s.bF[b], t);
+        const Body& bd = s.bd[lane];
+        double rb_[3] = {bd.c[0] - pB[0], bd.c[1] - pB[1], bd.c[2] - pB[2]}, t[3];
+        cross3(rb_, bd.F, t);
 #pragma unroll
-        for (int i = 0; i < 3; ++i) { s.contrib[b][i] = s.bF[b][i]; s.contrib[b][3 + i] = t[i] + s.bN[b][i]; }
+        for (int i = 0; i < 3; ++i) { s.contrib[lane][i] = bd.F[i]; s.contrib[lane][3 + i] = t[i] + bd.N[i]; }
     }
-    // U5: per joint: centroidal momentum column (about c), leg block of M, joint bias (C nu)_j
+    // stage C: per joint: centroidal momentum column (about c), leg block of M, joint bias (C nu)_j
     if (lane < 12) {
         const int j = lane, l = j / 3, k = j % 3;
         const double aj[3] = {s.ja[j][0], s.ja[j][1], s.ja[j][2]};
@@ -399,29 +428,29 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
         for (int kk = 0; kk < 3; ++kk) {
             if (kk >= k) {
                 const int b = 1 + 3 * l + kk;
-                const double mb = s.bm[b];
-                const double cb[3] = {s.bc[b][0], s.bc[b][1], s.bc[b][2]};
+                const double mb = md.link[l][kk].mass;
+                const Body& bd = s.bd[b];
+                const double cb[3] = {bd.c[0], bd.c[1], bd.c[2]};
                 double rel[3] = {cb[0] - oj[0], cb[1] - oj[1], cb[2] - oj[2]}, v[3], t[3], Ia[3], fm[3];
                 cross3(aj, rel, v);
                 double dc[3] = {cb[0] - c[0], cb[1] - c[1], cb[2] - c[2]};
                 cross3(dc, v, t);
-                mv3(s.bI[b], aj, Ia);
-                cross3(rel, s.bF[b], fm);
+                mv3(bd.I, aj, Ia);
+                cross3(rel, bd.F, fm);
 #pragma unroll
                 for (int i = 0; i < 3; ++i) {
                     Al[i] += mb * v[i];
                     Aa[i] += mb * t[i] + Ia[i];
-                    hsum[i] += fm[i] + s.bN[b][i];
+                    hsum[i] += fm[i] + bd.N[i];
                 }
 #pragma unroll
                 for (int k2 = 0; k2 < 3; ++k2) {
                     if (kk >= k2) {
                         const int j2 = 3 * l + k2;
                         const double a2[3] = {s.ja[j2][0], s.ja[j2][1], s.ja[j2][2]};
-                        double rel2[3] = {cb[0] - s.jo[j2][0], cb[1] - s.jo[j2][1], cb[2] - s.jo[j2][2]}, v2[3], Ia2[3];
+                        double rel2[3] = {cb[0] - s.jo[j2][0], cb[1] - s.jo[j2][1], cb[2] - s.jo[j2][2]}, v2[3];
                         cross3(a2, rel2, v2);
-                        mv3(s.bI[b], a2, Ia2);
-                        Mrow[k2] += mb * dot3(v, v2) + dot3(aj, Ia2);
+                        Mrow[k2] += mb * dot3(v, v2) + dot3(Ia, a2);
                     }
                 }
             }
@@ -436,6 +465,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
     }
     wsync();
     double hb[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll 1
     for (int b = 0; b < 13; ++b)
 #pragma unroll
         for (int k = 0; k < 6; ++k) hb[k] += s.contrib[b][k];
@@ -450,13 +480,14 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
         if (hvalid) {
             double yl = 0.0;
             if (lane < 6) {
+#pragma unroll
                 for (int cc = 0; cc < 18; ++cc) yl += H[H_TDINV + lane * 18 + cc] * s.in[7 + cc];
             }
 #pragma unroll
             for (int k = 0; k < 6; ++k) y[k] = bcast(yl, k);
         }
     }
-    // h' = C nu + M[:, 0:6] y ; M_bb = [[m I, -m S(r)], [m S(r), I_c - m S(r)^2]]
+    // h' = C nu + M[:, 0:6] y ; M_bb = [[m I, -m S(r)], [m S(r), I_c - m S(r)^2]] ; zeta = Mbar_b^-1 Ad^T h'_b
     double hp[6], zeta[6];
     {
         double t[3], u[3], w[3], Icy[3];
@@ -473,20 +504,24 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
         cross3(r, hp, t);
         hca[0] = hp[3] - t[0]; hca[1] = hp[4] - t[1]; hca[2] = hp[5] - t[2];
         zeta[0] = hp[0] * inv_m; zeta[1] = hp[1] * inv_m; zeta[2] = hp[2] * inv_m;
-        mv3(Icinv, hca, &zeta[3]);  // zeta = Mbar_b^-1 Ad^T h'_b
+        mv3(Icinv, hca, &zeta[3]);
     }
     if (lane == 0) {
+        double RB[9];
+        quat_R(s.in[3], s.in[4], s.in[5], s.in[6], RB);
         double* cen = s.cen;
-        cen[CEN_C] = c[0]; cen[CEN_C + 1] = c[1]; cen[CEN_C + 2] = c[2];
-        cen[CEN_CD] = cd[0]; cen[CEN_CD + 1] = cd[1]; cen[CEN_CD + 2] = cd[2];
-        cen[CEN_R] = r[0]; cen[CEN_R + 1] = r[1]; cen[CEN_R + 2] = r[2];
-        // currentPose_ = [c; eulAnglesRPY(R)] (cpp:262-264), centerOfMassVelocity_ = [c_dot; omega_B] (cpp:261)
-        cen[CEN_POSE] = c[0]; cen[CEN_POSE + 1] = c[1]; cen[CEN_POSE + 2] = c[2];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            cen[CEN_C + i] = c[i];
+            cen[CEN_CD + i] = cd[i];
+            cen[CEN_R + i] = r[i];
+            cen[CEN_POSE + i] = c[i];   // currentPose_ = [c; eulAnglesRPY(R)] (cpp:262-264)
+            cen[CEN_VC + i] = cd[i];    // centerOfMassVelocity_ = [c_dot; omega_B] (cpp:261, quirk A.4)
+            cen[CEN_VC + 3 + i] = wB[i];
+        }
         cen[CEN_POSE + 3] = atan2(RB[7], RB[8]);
         cen[CEN_POSE + 4] = atan2(-RB[6], sqrt(RB[7] * RB[7] + RB[8] * RB[8]));
         cen[CEN_POSE + 5] = atan2(RB[3], RB[0]);
-        cen[CEN_VC] = cd[0]; cen[CEN_VC + 1] = cd[1]; cen[CEN_VC + 2] = cd[2];
-        cen[CEN_VC + 3] = wB[0]; cen[CEN_VC + 4] = wB[1]; cen[CEN_VC + 5] = wB[2];
 #pragma unroll
         for (int i = 0; i < 6; ++i) cen[CEN_HB + i] = hp[i];
         P.m = m; P.inv_m = inv_m;
@@ -495,7 +530,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
     }
     const double dt = 1.0 / pr.loop_rate;
 
-    // U6/U7/U8: lane = joint column j: Jbar joint column, Mbar_j column, bbar_j
+    // lane = joint column j: Jbar joint column, Mbar_j column, bbar_j
     if (lane < 12) {
         const int j = lane, lj = j / 3, kj = j % 3;
         const double Alj[3] = {s.A[j][0], s.A[j][1], s.A[j][2]}, Aaj[3] = {s.A[j][3], s.A[j][4], s.A[j][5]};
@@ -510,6 +545,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
                 P.Jbj[(3 * l + rr) * 12 + j] = jf - Alj[rr] * inv_m + t[rr];
             }
         }
+#pragma unroll
         for (int i = 0; i < 12; ++i) {
             double Mij = (i / 3 == lj) ? s.Mjj[j][i % 3] : 0.0;
             Mij -= (s.A[i][0] * Alj[0] + s.A[i][1] * Alj[1] + s.A[i][2] * Alj[2]) * inv_m;
@@ -522,7 +558,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
         P.bbj[j] = hpj - (dot3(Alj, zeta) + dot3(Aaj, &zeta[3]));
         P.d[j] = s.pf[lj][kj] - sel3(c, kj);
     }
-    // U9: T_top = [Ad^-1(r), Mbar_b^-1 A_j]; Tdot_inv for the next cycle (cpp:291-293)
+    // T_top = [Ad^-1(r), Mbar_b^-1 A_j]; Tdot_inv for the next cycle (cpp:291-293)
     double tcol[6] = {0, 0, 0, 0, 0, 0};
     if (stateful) {
         double dr[3] = {0, 0, 0};
@@ -552,7 +588,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
             }
         }
     }
-    wsync();  // all reads of the old history and of U6 outputs done
+    wsync();  // all reads of the old history done
     if (stateful) {
         if (lane < 18) {
 #pragma unroll
@@ -567,7 +603,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
             }
         }
     }
-    // U10: finite-difference bounds (cpp:384-402, 503-515); swing commands (cpp:447-464)
+    // finite-difference bounds (cpp:384-402, 503-515); swing commands (cpp:447-464)
     if (lane < 12) {
         const int i = lane, l = i / 3, rr = i % 3;
         const double d[3] = {P.d[3 * l], P.d[3 * l + 1], P.d[3 * l + 2]};
@@ -575,6 +611,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
         double wxd[3];
         cross3(w3, d, wxd);
         double cur = s.cen[CEN_VC + rr] + sel3(wxd, rr);
+#pragma unroll
         for (int j = 0; j < 12; ++j) cur += P.Jbj[i * 12 + j] * qd[j];
         double old = 0.0;
         if (stateful && hvalid) {
@@ -582,6 +619,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
             double wxo[3];
             cross3(w3, dol, wxo);
             old = s.cen[CEN_VC + rr] + sel3(wxo, rr);
+#pragma unroll
             for (int j = 0; j < 12; ++j) old += H[H_JBJOLD + i * 12 + j] * qd[j];
         }
         const double kn = (kap >> l) & 1, ko = (kap_old >> l) & 1;
@@ -595,7 +633,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
         P.r1[i] = -jc_dot;
         P.rsw[i] = cmd - js_dot;
     }
-    // U11: desired wrench (cpp:426-445); integralError_ update after use (cpp:442)
+    // desired wrench (cpp:426-445); integralError_ update after use (cpp:442)
     if (lane < 6) {
         const int k = lane;
         const double kp = (k == 2) ? pr.kp_z : pr.kp;
@@ -604,8 +642,8 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
         if (k < 3) mba = m * ref[12 + k];
         else mba = P.Ic[3 * (k - 3)] * ref[15] + P.Ic[3 * (k - 3) + 1] * ref[16] + P.Ic[3 * (k - 3) + 2] * ref[17];
         const double e = s.cen[CEN_POSE + k] - ref[k];
-        const double Wk = -kp * e - pr.kd * (s.cen[CEN_VC + k] - ref[6 + k]) - pr.ki * eint + (k == 2 ? m * pr.gravity : 0.0) + mba;
-        P.W[k] = Wk;
+        P.W[k] = -kp * e - pr.kd * (s.cen[CEN_VC + k] - ref[6 + k]) - pr.ki * eint +
+                 (k == 2 ? md.total_mass * pr.gravity : 0.0) + mba;
         if (stateful) H[H_EINT + k] = eint + e / pr.loop_rate;
     }
     wsync();
@@ -625,22 +663,20 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
             D[WBC_DBG_POSE + lane] = s.cen[CEN_POSE + lane];
             D[WBC_DBG_VC + lane] = s.cen[CEN_VC + lane];
             D[WBC_DBG_WRENCH + lane] = P.W[lane];
-            // bbar_b = Ad^T h'_b (not used by the controller)
             const double* h6 = &s.cen[CEN_HB];
             double t[3];
             cross3(r, h6, t);
-            D[WBC_DBG_BBAR + lane] = (lane < 3) ? h6[lane] : h6[lane] - sel3(t, lane - 3);
+            D[WBC_DBG_BBAR + lane] = (lane < 3) ? h6[lane] : h6[lane] - sel3(t, lane - 3);  // Ad^T h'_b
         }
+        auto Sr = [&](int aa, int bb) -> double {  // S(r) entry
+            if (aa == bb) return 0.0;
+            if (aa == 0) return bb == 1 ? -r[2] : r[1];
+            if (aa == 1) return bb == 0 ? r[2] : -r[0];
+            return bb == 0 ? -r[1] : r[0];
+        };
         for (int e = lane; e < 324; e += 64) {
             const int i = e / 18, j = e % 18;
             double v;
-            // S(r) entry (a, b)
-            auto Sr = [&](int aa, int bb) -> double {
-                if (aa == bb) return 0.0;
-                if (aa == 0) return bb == 1 ? -r[2] : r[1];
-                if (aa == 1) return bb == 0 ? r[2] : -r[0];
-                return bb == 0 ? -r[1] : r[0];
-            };
             if (i < 6 && j < 6) {
                 if (i < 3 && j < 3) v = (i == j) ? m : 0.0;
                 else if (i < 3) v = -m * Sr(i, j - 3);
@@ -669,8 +705,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
             double v, vb;
             if (j < 3) {
                 v = vb = (rr == j) ? 1.0 : 0.0;
-            } else if (j < 6) {
-                // -S(p) e_(j-3) = e_(j-3) x p, row rr
+            } else if (j < 6) {  // -S(p) e = e x p, row rr
                 const double pfB[3] = {s.pf[l][0] - pB[0], s.pf[l][1] - pB[1], s.pf[l][2] - pB[2]};
                 const double dl[3] = {P.d[3 * l], P.d[3 * l + 1], P.d[3 * l + 2]};
                 double e3[3] = {j == 3 ? 1.0 : 0.0, j == 4 ? 1.0 : 0.0, j == 5 ? 1.0 : 0.0}, t[3], t2[3];
@@ -713,8 +748,8 @@ struct QpMap {
 
 __device__ __forceinline__ QpMap make_map(int kap) {
     QpMap q;
-    q.kap = kap;
-    q.ns = __builtin_popcount(kap & 15);
+    q.kap = kap & 15;
+    q.ns = __builtin_popcount(q.kap);
     q.nsw = 4 - q.ns;
     q.neq = 3 * q.ns;
     q.nfr = 4 * q.ns;
@@ -746,7 +781,7 @@ __device__ void build_normal(const Prob& P, const QpMap& mp, const wbc_params& p
     if (p >= mp.m) return;
     const double g0 = pr.gravity;
     const int kap = mp.kap;
-    // adds  Jc_com[l,k] Mbar_b^-1 Jc_com[mm,:]^T  to the stance slots (coefficient of f_mm):
+    // adds Jc_com[l,k] Mbar_b^-1 Jc_com[mm,:]^T to the stance slots (coefficient of f_mm):
     //   delta(k,rr)/m + (d_l x e_k) . I_c^-1 (d_mm x e_rr)
     auto slot_coupling = [&](int l, int k) {
         const double dl[3] = {P.d[3 * l], P.d[3 * l + 1], P.d[3 * l + 2]};
@@ -757,9 +792,8 @@ __device__ void build_normal(const Prob& P, const QpMap& mp, const wbc_params& p
         for (int mm = 0; mm < 4; ++mm) {
             if ((kap >> mm) & 1) {
                 const double dm[3] = {P.d[3 * mm], P.d[3 * mm + 1], P.d[3 * mm + 2]};
-                // (d_mm x e_rr) . v = e_rr . (v x d_mm)
                 double vx[3];
-                cross3(v, dm, vx);
+                cross3(v, dm, vx);  // (d_mm x e_rr) . v = e_rr . (v x d_mm)
 #pragma unroll
                 for (int rr = 0; rr < 3; ++rr) n[12 + 3 * mm + rr] += ((k == rr) ? P.inv_m : 0.0) + vx[rr];
             }
@@ -767,6 +801,7 @@ __device__ void build_normal(const Prob& P, const QpMap& mp, const wbc_params& p
     };
     if (p < mp.neq) {  // R1, stance rows: Jc_j qdd + Jc_com a = r1 with a = Mbar_b^-1 (Jc^T f - gw)
         const int l = nth_leg(kap, p / 3, 1), k = p % 3, i = 3 * l + k;
+#pragma unroll
         for (int j = 0; j < 12; ++j) n[j] = P.Jbj[i * 12 + j];
         slot_coupling(l, k);
         b = P.r1[i] + (k == 2 ? g0 : 0.0);
@@ -786,6 +821,7 @@ __device__ void build_normal(const Prob& P, const QpMap& mp, const wbc_params& p
     } else if (p < mp.neq + mp.nfr + mp.ntq) {  // R3 torque limits (cpp:495,506,513)
         const int q = p - mp.neq - mp.nfr, i = q / 2;
         const double sg = (q & 1) ? -1.0 : 1.0;
+#pragma unroll
         for (int j = 0; j < 12; ++j) n[j] = sg * P.Mbj[i * 12 + j];
 #pragma unroll
         for (int mm = 0; mm < 4; ++mm) {
@@ -798,6 +834,7 @@ __device__ void build_normal(const Prob& P, const QpMap& mp, const wbc_params& p
     } else {  // R4 / R5 swing rows (cpp:496-497,507-508,514-515)
         const int q = p - mp.neq - mp.nfr - mp.ntq, l = nth_leg(kap, q / 6, 0), k = (q % 6) / 2, i = 3 * l + k;
         const double sg = (q & 1) ? -1.0 : 1.0;  // +: w + s >= c' (R5) ; -: -w + s >= -c' (R4)
+#pragma unroll
         for (int j = 0; j < 12; ++j) n[j] = P.Jbj[i * 12 + j];
         slot_coupling(l, k);
 #pragma unroll
@@ -811,67 +848,59 @@ __device__ void build_normal(const Prob& P, const QpMap& mp, const wbc_params& p
     }
 }
 
-// C0[:, p] = J0^T n_p with J0 = blkdiag(I12, L^-T); also the initial slack n^T x0 - b
-__device__ void init_column(const QpScratch& s, const double* n, double b, double* cc, double& sp, double& nrm) {
-    double nn = 0.0, sx = 0.0;
-#pragma unroll
-    for (int k = 0; k < NQ; ++k) nn += n[k] * n[k];
+// C0[:, p] = J0^T n_p with J0 = blkdiag(I12, L^-T), in place: qdd part n, slot part L^-1 n_slot
+__device__ __forceinline__ void to_column(const QpScratch& s, double* cc) {
 #pragma unroll
     for (int k = 0; k < 12; ++k) {
-        cc[k] = n[k];
-        sx += n[12 + k] * s.xs[k];
-    }
+        double acc = cc[12 + k];
 #pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        double acc = 0.0;
-#pragma unroll
-        for (int i = 0; i <= k; ++i) acc += s.Linv[k][i] * n[12 + i];
-        cc[12 + k] = acc;
+        for (int i = 0; i < k; ++i) acc -= s.L[k][i] * cc[12 + i];
+        cc[12 + k] = acc / s.L[k][k];
     }
-    nrm = sqrt(fmax(nn, 1e-300));
-    sp = sx - b;
 }
 
-// Add the constraint whose column d is in s.dvec at position q: Householder on rows q..23 of every
-// lane's C column; R^-1 gains the column [-r / alpha; 1 / alpha] (rk = r of slot `lane`).
-__device__ __forceinline__ void add_column(QpScratch& s, int q, double zn, double rk, double* cc) {
+// d = C[:, p] broadcast from lane p (uniform, v_readlane)
+__device__ __forceinline__ void read_column(const double* cc, int p, double* d) {
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) d[k] = bcast(cc[k], p);
+}
+// r = R^-1 d[0:q] (slot lane i < q)
+__device__ __forceinline__ double rinv_times_d(const QpScratch& s, int q, const double* d) {
+    const int lane = lane_id();
+    const int i = lane < NQ ? lane : NQ - 1;
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+        const double v = s.Rinv[rp(i, j < i ? i : j)];
+        acc += (j >= lane && j < q) ? v * d[j] : 0.0;
+    }
+    return lane < q ? acc : 0.0;
+}
+// add the constraint with column d at position q: Householder on rows q..23 of every C column;
+// R^-1 gains the column [-r / alpha; 1 / alpha] (rk = r of slot `lane`)
+__device__ __forceinline__ void add_column(QpScratch& s, int q, double zn, double rk, const double* d, double* cc) {
     const int lane = lane_id();
     const double nrm2 = sqrt(zn);
-    const double dq = s.dvec[q];
+    double dq = 0.0;
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) dq = (k == q) ? d[k] : dq;
     const double alpha = (dq >= 0.0) ? -nrm2 : nrm2;
     const double beta = 1.0 / (nrm2 * (nrm2 + fabs(dq)));
     double vw = 0.0;
 #pragma unroll
     for (int k = 0; k < NQ; ++k) {
-        double vk = (k >= q) ? s.dvec[k] : 0.0;
-        if (k == q) vk -= alpha;
+        const double vk = (k > q) ? d[k] : ((k == q) ? d[k] - alpha : 0.0);
         vw += vk * cc[k];
     }
     vw *= beta;
 #pragma unroll
     for (int k = 0; k < NQ; ++k) {
-        double vk = (k >= q) ? s.dvec[k] : 0.0;
-        if (k == q) vk -= alpha;
+        const double vk = (k > q) ? d[k] : ((k == q) ? d[k] - alpha : 0.0);
         cc[k] -= vw * vk;
     }
     const double ia = 1.0 / alpha;
     if (lane < q) s.Rinv[rp(lane, q)] = -rk * ia;
     if (lane == q) s.Rinv[rp(q, q)] = ia;
-}
-
-__device__ __forceinline__ void load_d(QpScratch& s, int p, const double* cc) {
-    if (lane_id() == p) {
-#pragma unroll
-        for (int k = 0; k < NQ; ++k) s.dvec[k] = cc[k];
-    }
-    wsync();
-}
-__device__ __forceinline__ double rinv_times_d(const QpScratch& s, int q) {
-    const int lane = lane_id();
-    double acc = 0.0;
-    if (lane < q)
-        for (int j = lane; j < q; ++j) acc += s.Rinv[rp(lane, j)] * s.dvec[j];
-    return acc;
 }
 
 __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
@@ -892,69 +921,75 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
         if (wave_any(bad) && status == WBC_QP_OK) status = WBC_QP_INFEASIBLE;
     }
 
-    // slot Hessian H_s = I + Jc_com (I + Mbar_b^-2) Jc_com^T on stance slots, slack_weight I on swing slots
-    if (lane < 12) {
-        const int i = lane, li = i / 3, ri = i % 3;
-        const bool sti = (kap >> li) & 1;
-        const double di[3] = {P.d[3 * li], P.d[3 * li + 1], P.d[3 * li + 2]};
-        double e[3] = {ri == 0 ? 1.0 : 0.0, ri == 1 ? 1.0 : 0.0, ri == 2 ? 1.0 : 0.0}, ui[3];
-        cross3(di, e, ui);
-        double t[3], t2[3], Gu[3];
-        mv3(P.Icinv, ui, t);
-        mv3(P.Icinv, t, t2);
-        Gu[0] = ui[0] + t2[0]; Gu[1] = ui[1] + t2[1]; Gu[2] = ui[2] + t2[2];
-        for (int j = 0; j < 12; ++j) {
-            const int lj = j / 3, rj = j % 3;
-            const bool stj = (kap >> lj) & 1;
-            double h = 0.0;
-            if (sti && stj) {
+    // slot Hessian H_s = I + Jc_com (I + Mbar_b^-2) Jc_com^T on stance slots, slack_weight I on
+    // swing slots (lane i holds row i), its Cholesky factor in registers, x0 = -H^-1 g
+    {
+        double hrow[12];
+        double gsv = 0.0;
+        {
+            const int i = lane < 12 ? lane : 11, li = i / 3, ri = i % 3;
+            const bool sti = (kap >> li) & 1;
+            const double di[3] = {P.d[3 * li], P.d[3 * li + 1], P.d[3 * li + 2]};
+            double e[3] = {ri == 0 ? 1.0 : 0.0, ri == 1 ? 1.0 : 0.0, ri == 2 ? 1.0 : 0.0}, ui[3];
+            cross3(di, e, ui);
+            double t[3], t2[3], Gu[3];
+            mv3(P.Icinv, ui, t);
+            mv3(P.Icinv, t, t2);
+            Gu[0] = ui[0] + t2[0]; Gu[1] = ui[1] + t2[1]; Gu[2] = ui[2] + t2[2];
+            const double ims = 1.0 + inv_m * inv_m;
+#pragma unroll
+            for (int j = 0; j < 12; ++j) {
+                const int lj = j / 3, rj = j % 3;
+                const bool stj = (kap >> lj) & 1;
                 const double dj[3] = {P.d[3 * lj], P.d[3 * lj + 1], P.d[3 * lj + 2]};
                 double ej[3] = {rj == 0 ? 1.0 : 0.0, rj == 1 ? 1.0 : 0.0, rj == 2 ? 1.0 : 0.0}, uj[3];
                 cross3(dj, ej, uj);
-                h = (i == j ? 1.0 : 0.0) + (ri == rj ? 1.0 + inv_m * inv_m : 0.0) + dot3(Gu, uj);
-            } else if (!sti && i == j) {
-                h = pr.slack_weight;
+                const double h = (i == j ? 1.0 : 0.0) + (ri == rj ? ims : 0.0) + dot3(Gu, uj);
+                hrow[j] = (sti && stj) ? h : ((!sti && i == j) ? pr.slack_weight : 0.0);
             }
-            s.Hs[i][j] = h;
+            // g_s = -Jc_com (W + [0, 0, g/m, 0, 0, 0])
+            gsv = sti ? -(P.W[ri] + (ri == 2 ? pr.gravity * inv_m : 0.0) + dot3(ui, &P.W[3])) : 0.0;
         }
-        // g_s = -Jc_com (W + [0, 0, g/m, 0, 0, 0])
-        s.gs[i] = sti ? -(P.W[ri] + (ri == 2 ? pr.gravity * inv_m : 0.0) + dot3(ui, &P.W[3])) : 0.0;
-    }
-    wsync();
-    bool chol_ok = true;
-    for (int k = 0; k < 12; ++k) {  // H_s = L L^T, lane i owns row i
-        const double dkk = s.Hs[k][k];
-        if (!(dkk > 0.0)) chol_ok = false;
-        const double lkk = sqrt(fmax(dkk, 1e-300));
-        if (lane > k && lane < 12) s.Hs[lane][k] *= 1.0 / lkk;
-        wsync();
-        if (lane > k && lane < 12) {
-            const double lik = s.Hs[lane][k];
-            for (int j = k + 1; j <= lane; ++j) s.Hs[lane][j] -= lik * s.Hs[j][k];
+        // right-looking Cholesky, row i in lane i; L_jk broadcast with v_readlane
+        bool chol_ok = true;
+#pragma unroll
+        for (int k = 0; k < 12; ++k) {
+            const double dkk = bcast(hrow[k], k);
+            chol_ok &= dkk > 0.0;
+            const double lkk = sqrt(fmax(dkk, 1e-300));
+            const double il = 1.0 / lkk;
+            hrow[k] = (lane == k) ? lkk : hrow[k] * il;   // L_ik for lanes i > k
+#pragma unroll
+            for (int j = k + 1; j < 12; ++j) {
+                const double ljk = bcast(hrow[k], j);
+                if (lane >= j) hrow[j] -= hrow[k] * ljk;
+            }
         }
-        if (lane == k) s.Hs[k][k] = lkk;
-        wsync();
-    }
-    if (!chol_ok && status == WBC_QP_OK) status = WBC_QP_NUMERIC;
-    if (lane < 12) {  // Linv = L^-1, lane j solves L x = e_j
-        const int j = lane;
-        for (int i = 0; i < 12; ++i) {
-            double acc = (i == j) ? 1.0 : 0.0;
-            for (int k = j; k < i; ++k) acc -= s.Hs[i][k] * s.Linv[k][j];
-            s.Linv[i][j] = (i < j) ? 0.0 : acc / s.Hs[i][i];
+        if (!chol_ok && status == WBC_QP_OK) status = WBC_QP_NUMERIC;
+        if (lane < 12) {
+#pragma unroll
+            for (int j = 0; j < 12; ++j) s.L[lane][j] = (j <= lane) ? hrow[j] : 0.0;
         }
-    }
-    wsync();
-    if (lane < 12) {  // x0 = -H^-1 g, slot part: xs = -Linv^T (Linv g_s)
-        double acc = 0.0;
-        for (int i = 0; i <= lane; ++i) acc += s.Linv[lane][i] * s.gs[i];
-        s.tmp[lane] = acc;
-    }
-    wsync();
-    if (lane < 12) {
-        double acc = 0.0;
-        for (int k = lane; k < 12; ++k) acc += s.Linv[k][lane] * s.tmp[k];
-        s.xs[lane] = -acc;
+        // forward substitution L z = g_s (column-oriented; z_k from lane k)
+        double zk = 0.0;
+#pragma unroll
+        for (int k = 0; k < 12; ++k) {
+            const double zz = bcast(gsv / hrow[k], k);  // lane k: g_k' / L_kk
+            if (lane == k) zk = zz;
+            if (lane > k) gsv -= hrow[k] * zz;
+        }
+        wsync();  // L visible
+        // back substitution L^T x = z: lane j holds column j of L below the diagonal (L[k][j], k > j)
+        double lcol[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) lcol[k] = (lane < 12 && k > lane) ? s.L[k][lane] : 0.0;
+        double zt = zk;
+#pragma unroll
+        for (int k = 11; k >= 0; --k) {
+            const double xk = bcast(zt / hrow[k], k);  // lane k: (z_k - sum) / L_kk
+            if (lane == k) s.xs[k] = -xk;              // x0 = -H^-1 g
+            if (lane < k) zt -= lcol[k] * xk;
+        }
     }
     wsync();
 
@@ -964,62 +999,90 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
     bool is_eq = false, active = false;
     const bool is_con = lane < mp.m;
     {
-        double n[NQ];
-        build_normal(P, mp, pr, lane, n, bp, is_eq);
-        init_column(s, n, bp, cc, sp, nrm);
+        build_normal(P, mp, pr, lane, cc, bp, is_eq);
+        double nn = 0.0, sx = 0.0;
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) nn += cc[k] * cc[k];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) sx += cc[12 + k] * s.xs[k];
+        nrm = sqrt(fmax(nn, 1e-300));
+        sp = sx - bp;
+        to_column(s, cc);
     }
 
     STAMP(a, rb, 3);
-    // Goldfarb-Idnani (wave-uniform control flow)
+    // Goldfarb-Idnani (wave-uniform control flow).  After a drop the loop re-adds the remaining
+    // active set (rebuild mode) through the same add path, then resumes the pending constraint.
     int q = 0;         // active set size
     double u = 0.0;    // multiplier of active slot `lane`
     int act = -1;      // constraint id of active slot `lane`
     int neq_added = 0; // equalities occupy slots 0..neq_added-1
     int next_eq = 0;
     int pstar = -1;
+    int rbk = -1;      // rebuild cursor (>= 0 while re-adding active slot rbk)
     double up = 0.0;
     const double tiny = 1e-26;
     bool done = (status != WBC_QP_OK);
 
     while (!done) {
+        if (rbk >= q) rbk = -1;  // rebuild finished
+        const bool rebuild = rbk >= 0;
         bool eq_step = false;
-        if (pstar < 0) {
-            if (next_eq < mp.neq) {
-                pstar = next_eq++;
-                eq_step = true;
-            } else {
-                double v = 1e300;
-                if (is_con && !is_eq && !active) {
-                    const double tol = 1e-10 * fmax(1.0, fabs(bp));
-                    if (sp < -tol) v = sp / nrm;
+        int col, pos;
+        if (rebuild) {
+            col = bcast_i(act, rbk);
+            pos = rbk;
+        } else {
+            if (pstar < 0) {
+                if (next_eq < mp.neq) {
+                    pstar = next_eq++;
+                    eq_step = true;
+                } else {
+                    double v = 1e300;
+                    if (is_con && !is_eq && !active) {
+                        const double tol = 1e-10 * fmax(1.0, fabs(bp));
+                        if (sp < -tol) v = sp / nrm;
+                    }
+                    int idx = lane;
+                    wave_argmin(v, idx);
+                    if (!(v < 1e299)) break;  // no violated constraint: optimal
+                    pstar = idx;
                 }
-                int idx = lane;
-                wave_argmin(v, idx);
-                if (!(v < 1e299)) break;  // no violated constraint: optimal
-                pstar = idx;
+                up = 0.0;
             }
-            up = 0.0;
+            if (!eq_step) {
+                if (++iters > pr.max_wsr) { status = WBC_QP_MAX_ITER; iters = pr.max_wsr; break; }
+            }
+            col = pstar;
+            pos = q;
         }
-        if (!eq_step) {
-            if (++iters > pr.max_wsr) { status = WBC_QP_MAX_ITER; iters = pr.max_wsr; break; }
-        }
-        load_d(s, pstar, cc);
-        const double rk = rinv_times_d(s, q);
+        double d[NQ];
+        read_column(cc, col, d);
+        const double rk = rinv_times_d(s, pos, d);
         double zn = 0.0, cz = 0.0;
 #pragma unroll
         for (int k = 0; k < NQ; ++k) {
-            const double dk = (k >= q) ? s.dvec[k] : 0.0;
+            const double dk = (k >= pos) ? d[k] : 0.0;
             zn += dk * dk;
             cz += cc[k] * dk;  // (C2^T d2)_p = n_p^T z
         }
+        if (rebuild) {
+            add_column(s, pos, zn, rk, d, cc);
+            ++rbk;
+            wsync();
+            continue;
+        }
         const double sps = bcast(sp, pstar);
-        if (eq_step && zn <= tiny * fmax(1.0, bcast(nrm, pstar) * bcast(nrm, pstar))) {
-            if (fabs(sps) <= 1e-9 * fmax(1.0, fabs(bcast(bp, pstar)))) {  // redundant, consistent
-                pstar = -1;
-                continue;
+        if (eq_step) {
+            const double np2 = bcast(nrm, pstar);
+            if (zn <= tiny * fmax(1.0, np2 * np2)) {
+                if (fabs(sps) <= 1e-9 * fmax(1.0, fabs(bcast(bp, pstar)))) {  // redundant, consistent
+                    pstar = -1;
+                    continue;
+                }
+                status = WBC_QP_INFEASIBLE;
+                break;
             }
-            status = WBC_QP_INFEASIBLE;
-            break;
         }
         double t1 = 1e300;
         int l1 = 64;
@@ -1038,7 +1101,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
         if (lane < q) u -= t * rk;
         up += t;
         if (full) {
-            add_column(s, q, zn, rk, cc);
+            add_column(s, q, zn, rk, d, cc);
             if (lane == q) { u = up; act = pstar; }
             if (lane == pstar) active = true;
             ++q;
@@ -1046,70 +1109,76 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
             pstar = -1;
             wsync();
         } else {
-            // drop active slot l1: shift the active list, rebuild C and R^-1 by re-adding the rest
+            // drop active slot l1: shift the active list; C restarts from C0 and the rest is re-added
             const int l = l1;
             const int dropped = bcast_i(act, l);
             if (lane == dropped) active = false;
-            {
-                const double un = __shfl(u, (lane + 1) & 63);
-                const int an = __shfl(act, (lane + 1) & 63);
-                if (lane >= l && lane < q - 1) { u = un; act = an; }
-                if (lane == q - 1) { u = 0.0; act = -1; }
-            }
+            const double un = __shfl(u, (lane + 1) & 63);
+            const int an = __shfl(act, (lane + 1) & 63);
+            if (lane >= l && lane < q - 1) { u = un; act = an; }
+            if (lane == q - 1) { u = 0.0; act = -1; }
             --q;
-            double n[NQ], bb, spd, nd;
+            double bb;
             bool eqd;
-            build_normal(P, mp, pr, lane, n, bb, eqd);
-            init_column(s, n, bb, cc, spd, nd);  // fresh C0; slacks sp are kept
-            for (int k = 0; k < q; ++k) {
-                const int pk = bcast_i(act, k);
-                load_d(s, pk, cc);
-                const double rkk = rinv_times_d(s, k);
-                double znk = 0.0;
-#pragma unroll
-                for (int j = 0; j < NQ; ++j) {
-                    const double dj = (j >= k) ? s.dvec[j] : 0.0;
-                    znk += dj * dj;
-                }
-                add_column(s, k, znk, rkk, cc);
-                wsync();
-            }
-            // keep pstar (its slack was advanced); loop re-evaluates the step for it
+            build_normal(P, mp, pr, lane, cc, bb, eqd);
+            to_column(s, cc);  // fresh C0; slacks sp are kept
+            rbk = 0;
+            // pstar stays pending (its slack was advanced)
         }
     }
 
     STAMP(a, rb, 4);
-    // primal recovery: y = x0 + H^-1 sum_k u_k n_{a_k}
-    if (lane < 64) s.ucon[lane] = 0.0;
+    // primal recovery: y = x0 + H^-1 w,  w = sum_k u_k n_{a_k}  (LDS transpose-sum over active rows)
+    if (lane < 64) s.ucon[lane] = -1.0;  // slot index of constraint `lane` (or -1)
     wsync();
-    if (lane < q && act >= 0) s.ucon[act] = u;
+    if (lane < q && act >= 0) s.ucon[act] = (double)lane;
     wsync();
-    double w[NQ];
     {
-        double n[NQ], bb;
-        bool eqf;
-        build_normal(P, mp, pr, lane, n, bb, eqf);
-        const double uc = is_con ? s.ucon[lane] : 0.0;
+        const int slot = is_con ? (int)s.ucon[lane] : -1;
+        const double uk = __shfl(u, slot < 0 ? 0 : slot);  // multiplier held by the slot lane
+        if (slot >= 0) {
+            double n[NQ], bb;
+            bool eqf;
+            build_normal(P, mp, pr, lane, n, bb, eqf);
 #pragma unroll
-        for (int k = 0; k < NQ; ++k) w[k] = wave_sum(uc * n[k]);
-    }
-    if (lane < 12) {
-        double acc = 0.0;
-#pragma unroll
-        for (int i = 0; i < 12; ++i)
-            if (i <= lane) acc += s.Linv[lane][i] * w[12 + i];
-        s.tmp[lane] = acc;
+            for (int k = 0; k < NQ; ++k) s.Wt[slot][k] = uk * n[k];
+        }
     }
     wsync();
-    if (lane < 12) {
-        double acc = 0.0;
-        for (int k = lane; k < 12; ++k) acc += s.Linv[k][lane] * s.tmp[k];
-        s.dvec[12 + lane] = s.xs[lane] + acc;  // slot part of y
-    }
-    if (lane == 0) {
+    double wi = 0.0;  // w_i for lane i < 24
+    if (lane < NQ) {
 #pragma unroll
-        for (int k = 0; k < 12; ++k) s.dvec[k] = w[k];  // qdd part of y
+        for (int k = 0; k < NQ; ++k) wi += (k < q) ? s.Wt[k][lane] : 0.0;
     }
+    // slots: y_s = xs + L^-T L^-1 w_s (lane i < 12 handles row i of the slot block, w_s[i] = w_{12+i})
+    double ws = __shfl(wi, (lane + 12) & 63);
+    double yv;
+    {
+        double lrow[12], lcol[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) {
+            lrow[k] = (lane < 12 && k <= lane) ? s.L[lane][k] : 1.0;
+            lcol[k] = (lane < 12 && k > lane) ? s.L[k][lane] : 0.0;
+        }
+        double zk = 0.0;
+#pragma unroll
+        for (int k = 0; k < 12; ++k) {
+            const double zz = bcast(ws / lrow[k], k);  // lane k: (w_k - sum) / L_kk
+            if (lane == k) zk = zz;
+            if (lane > k) ws -= lrow[k] * zz;
+        }
+        double zt = zk, xk_own = 0.0;
+#pragma unroll
+        for (int k = 11; k >= 0; --k) {
+            const double xk = bcast(zt / lrow[k], k);
+            if (lane == k) xk_own = xk;
+            if (lane < k) zt -= lcol[k] * xk;
+        }
+        yv = (lane < 12) ? s.xs[lane < 12 ? lane : 0] + xk_own : 0.0;
+    }
+    wsync();  // Wt (aliases Rinv) and ucon fully consumed
+    double* yq = s.ucon;  // y[0..23]: qdd (w[0:12]) then slots
+    if (lane < 12) { yq[lane] = wi; yq[12 + lane] = yv; }
     wsync();
 
     STAMP(a, rb, 5);
@@ -1122,7 +1191,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
 #pragma unroll
             for (int l = 0; l < 4; ++l) {
                 if ((kap >> l) & 1) {
-                    const double fl[3] = {s.dvec[12 + 3 * l], s.dvec[13 + 3 * l], s.dvec[14 + 3 * l]};
+                    const double fl[3] = {yq[12 + 3 * l], yq[13 + 3 * l], yq[14 + 3 * l]};
                     const double dl[3] = {P.d[3 * l], P.d[3 * l + 1], P.d[3 * l + 2]};
                     double t[3];
                     cross3(dl, fl, t);
@@ -1136,23 +1205,24 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
                 xv = P.Icinv[3 * rr] * Mm[0] + P.Icinv[3 * rr + 1] * Mm[1] + P.Icinv[3 * rr + 2] * Mm[2];
             }
         } else if (lane < 18) {
-            xv = s.dvec[lane - 6];
+            xv = yq[lane - 6];
         } else if (lane < 30) {
             const int i = lane - 18;
-            xv = ((kap >> (i / 3)) & 1) ? s.dvec[12 + i] : 0.0;
+            xv = ((kap >> (i / 3)) & 1) ? yq[12 + i] : 0.0;
         } else {
             const int i = lane - 30;
-            xv = ((kap >> (i / 3)) & 1) ? fabs(P.rsw[i]) : s.dvec[12 + i];
+            xv = ((kap >> (i / 3)) & 1) ? fabs(P.rsw[i]) : yq[12 + i];
         }
         if (a.x) a.x[(size_t)rb * WBC_NV + lane] = ok ? xv : 0.0;
     }
     if (lane < 12) {
         double tv = P.bbj[lane];
+#pragma unroll
         for (int i = 0; i < 12; ++i) {
-            const double fi = ((kap >> (i / 3)) & 1) ? s.dvec[12 + i] : 0.0;
-            tv += P.Mbj[lane * 12 + i] * s.dvec[i] - P.Jbj[i * 12 + lane] * fi;
+            const double fi = ((kap >> (i / 3)) & 1) ? yq[12 + i] : 0.0;
+            tv += P.Mbj[lane * 12 + i] * yq[i] - P.Jbj[i * 12 + lane] * fi;
         }
-        const double fl = ((kap >> (lane / 3)) & 1) ? s.dvec[12 + lane] : 0.0;
+        const double fl = ((kap >> (lane / 3)) & 1) ? yq[12 + lane] : 0.0;
         a.tau[(size_t)rb * 12 + lane] = ok ? tv : 0.0;
         a.grf[(size_t)rb * 12 + lane] = ok ? fl : 0.0;
     }
@@ -1163,9 +1233,12 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
 }
 
 // ---------------------------------------------------------------------------------------
-// kernels
+// kernels: one 64-lane workgroup per robot
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64, WBC_WAVES_PER_SIMD) void wbc_step_kernel(KernelArgs a) {
+#define WBC_KERNEL_ATTR \
+    __global__ __attribute__((amdgpu_flat_work_group_size(64, 64), amdgpu_waves_per_eu(WBC_WAVES_PER_SIMD)))
+
+WBC_KERNEL_ATTR void wbc_step_kernel(KernelArgs a) {
     __shared__ Lds L;
     const int rb = blockIdx.x;
     if (rb >= a.batch) return;
@@ -1176,7 +1249,7 @@ __global__ __launch_bounds__(64, WBC_WAVES_PER_SIMD) void wbc_step_kernel(Kernel
     STAMP(a, rb, 6);
 }
 
-__global__ __launch_bounds__(64, WBC_WAVES_PER_SIMD) void wbc_update_kernel(KernelArgs a) {
+WBC_KERNEL_ATTR void wbc_update_kernel(KernelArgs a) {
     __shared__ Lds L;
     const int rb = blockIdx.x;
     if (rb >= a.batch) return;
@@ -1186,7 +1259,7 @@ __global__ __launch_bounds__(64, WBC_WAVES_PER_SIMD) void wbc_update_kernel(Kern
     for (int k = lane_id(); k < PROB_LEN; k += 64) dst[k] = src[k];
 }
 
-__global__ __launch_bounds__(64, WBC_WAVES_PER_SIMD) void wbc_solve_kernel(KernelArgs a) {
+WBC_KERNEL_ATTR void wbc_solve_kernel(KernelArgs a) {
     __shared__ Lds L;
     const int rb = blockIdx.x;
     if (rb >= a.batch) return;
