@@ -59,6 +59,14 @@ def load_library(path: str = LIB_PATH):
         return _lib
     if not os.path.exists(path):
         raise OSError(f"HIP engine library not built: {path} (run __graft_entry__.build())")
+    # One HIP runtime per process: torch bundles its own libamdhip64 (soname libamdhip64.so.7,
+    # requested as "libamdhip64.so").  Loaded first, it satisfies our DT_NEEDED
+    # libamdhip64.so.7 and both share it; loaded after us, it would be mapped a second time and
+    # torch's device init fails ("No HIP GPUs are available").
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(path)
     P, I32, U32 = C.c_void_p, C.c_int32, C.c_uint32
     dp = C.POINTER(C.c_double)

@@ -33,7 +33,6 @@
 namespace wbc {
 
 constexpr int NQ = 24;                  // reduced QP variables
-constexpr int RPACK = NQ * (NQ + 1) / 2;
 
 struct Frame {  // world frame of a body after stage A
     double R[9], o[3], w[3], al[3], ao[3], vo[3];
@@ -68,7 +67,9 @@ struct QpScratch {
     double xs[12];          // slot part of x0 = -H^-1 g
     double ucon[64];
     union {
-        double Rinv[RPACK];  // packed upper-triangular R^-1, column-major: (i,j) -> j(j+1)/2 + i
+        // R^-1 (upper triangular, zero elsewhere): element (i, j) at Rv[j / 2][i].{x, y}[j % 2], so
+        // lane i reads its row as 12 conflict-free ds_read_b128 and R^-1 d needs no masking
+        double2 Rv[NQ / 2][NQ];
         double Wt[NQ][NQ];   // primal recovery: row k = u_k n_{a_k}
     };
 };
@@ -850,12 +851,16 @@ __device__ void build_normal(const Prob& P, const QpMap& mp, const wbc_params& p
 
 // C0[:, p] = J0^T n_p with J0 = blkdiag(I12, L^-T), in place: qdd part n, slot part L^-1 n_slot
 __device__ __forceinline__ void to_column(const QpScratch& s, double* cc) {
+    // compiler barrier: keeps the L reads here (inside the active-set loop, on the rare drop path)
+    // instead of letting LICM hoist all 78 of them into registers for the whole loop
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (int k = 0; k < 12; ++k) {
         double acc = cc[12 + k];
 #pragma unroll
         for (int i = 0; i < k; ++i) acc -= s.L[k][i] * cc[12 + i];
         cc[12 + k] = acc / s.L[k][k];
+        __builtin_amdgcn_sched_barrier(0);  // one row of L in flight, not all 78 entries
     }
 }
 
@@ -864,43 +869,48 @@ __device__ __forceinline__ void read_column(const double* cc, int p, double* d) 
 #pragma unroll
     for (int k = 0; k < NQ; ++k) d[k] = bcast(cc[k], p);
 }
-// r = R^-1 d[0:q] (slot lane i < q)
-__device__ __forceinline__ double rinv_times_d(const QpScratch& s, int q, const double* d) {
+__device__ __forceinline__ void zero_rinv(QpScratch& s) {
+    double2* r = &s.Rv[0][0];
     const int lane = lane_id();
-    const int i = lane < NQ ? lane : NQ - 1;
+#pragma unroll
+    for (int k = 0; k < (NQ / 2) * NQ; k += 64)
+        if (k + lane < (NQ / 2) * NQ) r[k + lane] = make_double2(0.0, 0.0);
+}
+// r = R^-1 d (lane i < q holds r_i; rows >= q and columns >= q of R^-1 are zero)
+__device__ __forceinline__ double rinv_times_d(const QpScratch& s, const double* d) {
+    const int lane = lane_id();
+    const int i = lane < NQ ? lane : 0;
     double acc = 0.0;
 #pragma unroll
-    for (int j = 0; j < NQ; ++j) {
-        const double v = s.Rinv[rp(i, j < i ? i : j)];
-        acc += (j >= lane && j < q) ? v * d[j] : 0.0;
+    for (int jj = 0; jj < NQ / 2; ++jj) {
+        const double2 v = s.Rv[jj][i];
+        acc += v.x * d[2 * jj];
+        acc += v.y * d[2 * jj + 1];
     }
-    return lane < q ? acc : 0.0;
+    return lane < NQ ? acc : 0.0;
 }
-// add the constraint with column d at position q: Householder on rows q..23 of every C column;
-// R^-1 gains the column [-r / alpha; 1 / alpha] (rk = r of slot `lane`)
-__device__ __forceinline__ void add_column(QpScratch& s, int q, double zn, double rk, const double* d, double* cc) {
+// add the constraint with column d at position q: Householder on rows q..23 of every C column
+// (v = d with rows < q zeroed on entry, the Householder vector on exit; dq = d[q]); R^-1 gains the column [-r / alpha; 1 / alpha]
+__device__ __forceinline__ void add_column(QpScratch& s, int q, double zn, double dq, double rk, double* v,
+                                           double* cc) {
     const int lane = lane_id();
     const double nrm2 = sqrt(zn);
-    double dq = 0.0;
-#pragma unroll
-    for (int k = 0; k < NQ; ++k) dq = (k == q) ? d[k] : dq;
     const double alpha = (dq >= 0.0) ? -nrm2 : nrm2;
     const double beta = 1.0 / (nrm2 * (nrm2 + fabs(dq)));
+    const double vq = dq - alpha;
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) v[k] = (k == q) ? vq : v[k];  // in place: d2 -> Householder vector
     double vw = 0.0;
 #pragma unroll
-    for (int k = 0; k < NQ; ++k) {
-        const double vk = (k > q) ? d[k] : ((k == q) ? d[k] - alpha : 0.0);
-        vw += vk * cc[k];
-    }
+    for (int k = 0; k < NQ; ++k) vw += v[k] * cc[k];
     vw *= beta;
 #pragma unroll
-    for (int k = 0; k < NQ; ++k) {
-        const double vk = (k > q) ? d[k] : ((k == q) ? d[k] - alpha : 0.0);
-        cc[k] -= vw * vk;
-    }
+    for (int k = 0; k < NQ; ++k) cc[k] -= vw * v[k];
     const double ia = 1.0 / alpha;
-    if (lane < q) s.Rinv[rp(lane, q)] = -rk * ia;
-    if (lane == q) s.Rinv[rp(q, q)] = ia;
+    if (lane <= q) {
+        double* col = reinterpret_cast<double*>(&s.Rv[q >> 1][lane]) + (q & 1);
+        *col = (lane == q) ? ia : -rk * ia;
+    }
 }
 
 __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
@@ -1010,6 +1020,8 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
         to_column(s, cc);
     }
 
+    zero_rinv(s);
+    wsync();
     STAMP(a, rb, 3);
     // Goldfarb-Idnani (wave-uniform control flow).  After a drop the loop re-adds the remaining
     // active set (rebuild mode) through the same add path, then resumes the pending constraint.
@@ -1025,6 +1037,9 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
     bool done = (status != WBC_QP_OK);
 
     while (!done) {
+        // compiler barrier: LDS reads of the problem (build_normal / to_column on the rare drop
+        // path) stay inside the loop instead of being hoisted into registers for its whole length
+        asm volatile("" ::: "memory");
         if (rbk >= q) rbk = -1;  // rebuild finished
         const bool rebuild = rbk >= 0;
         bool eq_step = false;
@@ -1058,16 +1073,19 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
         }
         double d[NQ];
         read_column(cc, col, d);
-        const double rk = rinv_times_d(s, pos, d);
-        double zn = 0.0, cz = 0.0;
+        const double rk = rinv_times_d(s, d);
+        double dq = 0.0;
 #pragma unroll
         for (int k = 0; k < NQ; ++k) {
-            const double dk = (k >= pos) ? d[k] : 0.0;
-            zn += dk * dk;
-            cz += cc[k] * dk;  // (C2^T d2)_p = n_p^T z
+            dq = (k == pos) ? d[k] : dq;
+            d[k] = (k >= pos) ? d[k] : 0.0;  // d2 (rows >= pos)
         }
+        double cz = 0.0;
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) cz += cc[k] * d[k];  // (C2^T d2)_p = n_p^T z
+        const double zn = bcast(cz, col);                   // |d2|^2: lane col holds d itself
         if (rebuild) {
-            add_column(s, pos, zn, rk, d, cc);
+            add_column(s, pos, zn, dq, rk, d, cc);
             ++rbk;
             wsync();
             continue;
@@ -1101,7 +1119,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
         if (lane < q) u -= t * rk;
         up += t;
         if (full) {
-            add_column(s, q, zn, rk, d, cc);
+            add_column(s, q, zn, dq, rk, d, cc);
             if (lane == q) { u = up; act = pstar; }
             if (lane == pstar) active = true;
             ++q;
@@ -1122,6 +1140,9 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
             bool eqd;
             build_normal(P, mp, pr, lane, cc, bb, eqd);
             to_column(s, cc);  // fresh C0; slacks sp are kept
+            wsync();
+            zero_rinv(s);
+            wsync();
             rbk = 0;
             // pstar stays pending (its slack was advanced)
         }
