@@ -1,7 +1,8 @@
 // wbc_kernel.hip — batched whole-body-control step for gfx950 (MI355X), fp64.
 //
-// One robot per 64-lane wavefront (one workgroup = one wave); 16 robots per CU (4 waves per
-// SIMD: <= 128 VGPRs, <= 10 KB of LDS per robot), so a 4096-robot batch is one pass of the chip.
+// One robot per 64-lane wavefront (one workgroup = one wave).  Default occupancy: 2 waves per
+// SIMD (<= 256 VGPRs, spill-free; 8 robots per CU, ~9.6 KB of LDS per robot); the 4-wave build
+// (<= 128 VGPRs) spills and is slower (profiles/r01/variants_*.log).
 //
 //   update (≙ WholeBodyController::updateState, src/whole_body_controller.cpp:256-294)
 //     stage A  lanes 0..11 = joints: sin/cos; lanes 0..3 = legs: forward kinematics chain
@@ -27,7 +28,7 @@
 #include "wbc_layout.h"
 
 #ifndef WBC_WAVES_PER_SIMD
-#define WBC_WAVES_PER_SIMD 4
+#define WBC_WAVES_PER_SIMD 2
 #endif
 
 namespace wbc {
@@ -851,16 +852,12 @@ __device__ void build_normal(const Prob& P, const QpMap& mp, const wbc_params& p
 
 // C0[:, p] = J0^T n_p with J0 = blkdiag(I12, L^-T), in place: qdd part n, slot part L^-1 n_slot
 __device__ __forceinline__ void to_column(const QpScratch& s, double* cc) {
-    // compiler barrier: keeps the L reads here (inside the active-set loop, on the rare drop path)
-    // instead of letting LICM hoist all 78 of them into registers for the whole loop
-    asm volatile("" ::: "memory");
 #pragma unroll
     for (int k = 0; k < 12; ++k) {
         double acc = cc[12 + k];
 #pragma unroll
         for (int i = 0; i < k; ++i) acc -= s.L[k][i] * cc[12 + i];
         cc[12 + k] = acc / s.L[k][k];
-        __builtin_amdgcn_sched_barrier(0);  // one row of L in flight, not all 78 entries
     }
 }
 
@@ -891,9 +888,10 @@ __device__ __forceinline__ double rinv_times_d(const QpScratch& s, const double*
 }
 // add the constraint with column d at position q: Householder on rows q..23 of every C column
 // (v = d with rows < q zeroed on entry, the Householder vector on exit; dq = d[q]); R^-1 gains the column [-r / alpha; 1 / alpha]
-__device__ __forceinline__ void add_column(QpScratch& s, int q, double zn, double dq, double rk, double* v,
-                                           double* cc) {
+__device__ __forceinline__ void add_column(QpScratch& s, int q, bool add, double zn, double dq, double rk,
+                                           double* v, double* cc) {
     const int lane = lane_id();
+    if (!add) { zn = 1.0; dq = 0.0; }  // no-op update: vw = 0 below leaves cc bit-identical
     const double nrm2 = sqrt(zn);
     const double alpha = (dq >= 0.0) ? -nrm2 : nrm2;
     const double beta = 1.0 / (nrm2 * (nrm2 + fabs(dq)));
@@ -903,11 +901,11 @@ __device__ __forceinline__ void add_column(QpScratch& s, int q, double zn, doubl
     double vw = 0.0;
 #pragma unroll
     for (int k = 0; k < NQ; ++k) vw += v[k] * cc[k];
-    vw *= beta;
+    vw = add ? vw * beta : 0.0;
 #pragma unroll
     for (int k = 0; k < NQ; ++k) cc[k] -= vw * v[k];
     const double ia = 1.0 / alpha;
-    if (lane <= q) {
+    if (add && lane <= q) {
         double* col = reinterpret_cast<double*>(&s.Rv[q >> 1][lane]) + (q & 1);
         *col = (lane == q) ? ia : -rk * ia;
     }
@@ -1084,67 +1082,82 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
 #pragma unroll
         for (int k = 0; k < NQ; ++k) cz += cc[k] * d[k];  // (C2^T d2)_p = n_p^T z
         const double zn = bcast(cz, col);                   // |d2|^2: lane col holds d itself
-        if (rebuild) {
-            add_column(s, pos, zn, dq, rk, d, cc);
-            ++rbk;
-            wsync();
-            continue;
-        }
-        const double sps = bcast(sp, pstar);
-        if (eq_step) {
-            const double np2 = bcast(nrm, pstar);
-            if (zn <= tiny * fmax(1.0, np2 * np2)) {
-                if (fabs(sps) <= 1e-9 * fmax(1.0, fabs(bcast(bp, pstar)))) {  // redundant, consistent
-                    pstar = -1;
-                    continue;
+
+        // step (skipped in rebuild mode: the active set is re-added as is)
+        bool add = true, drop = false;
+        if (!rebuild) {
+            const double sps = bcast(sp, pstar);
+            if (eq_step) {
+                const double np2 = bcast(nrm, pstar);
+                if (zn <= tiny * fmax(1.0, np2 * np2)) {
+                    if (!(fabs(sps) <= 1e-9 * fmax(1.0, fabs(bcast(bp, pstar))))) {
+                        status = WBC_QP_INFEASIBLE;
+                        break;
+                    }
+                    add = false;  // redundant, consistent equality: nothing to add
                 }
-                status = WBC_QP_INFEASIBLE;
-                break;
+            }
+            double t1 = 1e300;
+            int l1 = 64;
+            if (!eq_step) {  // partial step: keep active inequality multipliers >= 0
+                double v = 1e300;
+                if (lane < q && lane >= neq_added && rk > 1e-14) v = u / rk;
+                l1 = lane;
+                wave_argmin(v, l1);
+                t1 = v;
+            }
+            if (add) {
+                const double t2 = (zn > tiny) ? (-sps / zn) : 1e300;
+                const double t = eq_step ? t2 : fmin(t1, t2);
+                if (!(t < 1e299)) { status = WBC_QP_INFEASIBLE; break; }
+                const bool full = eq_step || (t2 < 1e299 && t2 <= t1);
+                if (t2 < 1e299) sp += t * cz;
+                if (lane < q) u -= t * rk;
+                up += t;
+                if (!full) {
+                    add = false;
+                    drop = true;
+                    // drop active slot l1: shift the active list
+                    const int dropped = bcast_i(act, l1);
+                    if (lane == dropped) active = false;
+                    const double un = __shfl(u, (lane + 1) & 63);
+                    const int an = __shfl(act, (lane + 1) & 63);
+                    if (lane >= l1 && lane < q - 1) { u = un; act = an; }
+                    if (lane == q - 1) { u = 0.0; act = -1; }
+                    --q;
+                    // pstar stays pending (its slack was advanced)
+                }
+            } else {
+                pstar = -1;
             }
         }
-        double t1 = 1e300;
-        int l1 = 64;
-        if (!eq_step) {  // partial step: keep active inequality multipliers >= 0
-            double v = 1e300;
-            if (lane < q && lane >= neq_added && rk > 1e-14) v = u / rk;
-            l1 = lane;
-            wave_argmin(v, l1);
-            t1 = v;
-        }
-        const double t2 = (zn > tiny) ? (-sps / zn) : 1e300;
-        const double t = eq_step ? t2 : fmin(t1, t2);
-        if (!(t < 1e299)) { status = WBC_QP_INFEASIBLE; break; }
-        const bool full = eq_step || (t2 < 1e299 && t2 <= t1);
-        if (t2 < 1e299) sp += t * cz;
-        if (lane < q) u -= t * rk;
-        up += t;
-        if (full) {
-            add_column(s, q, zn, dq, rk, d, cc);
-            if (lane == q) { u = up; act = pstar; }
-            if (lane == pstar) active = true;
-            ++q;
-            if (eq_step) neq_added = q;
-            pstar = -1;
+        // one in-place update site for every path (no second live copy of cc)
+        add_column(s, pos, add, zn, dq, rk, d, cc);
+        if (add) {
+            if (rebuild) {
+                ++rbk;
+            } else {
+                if (lane == q) { u = up; act = pstar; }
+                if (lane == pstar) active = true;
+                ++q;
+                if (eq_step) neq_added = q;
+                pstar = -1;
+            }
             wsync();
-        } else {
-            // drop active slot l1: shift the active list; C restarts from C0 and the rest is re-added
-            const int l = l1;
-            const int dropped = bcast_i(act, l);
-            if (lane == dropped) active = false;
-            const double un = __shfl(u, (lane + 1) & 63);
-            const int an = __shfl(act, (lane + 1) & 63);
-            if (lane >= l && lane < q - 1) { u = un; act = an; }
-            if (lane == q - 1) { u = 0.0; act = -1; }
-            --q;
+        }
+        if (drop) {
+            // C restarts from C0 and the remaining active set is re-added (rebuild mode).
+            // Opaque copy of the lane id: the constraint decode inside build_normal must not be
+            // hoisted out of the loop (LICM would keep ~40 per-lane invariants live in VGPRs).
             double bb;
             bool eqd;
-            build_normal(P, mp, pr, lane, cc, bb, eqd);
+            int pl = lane;
+            asm volatile("" : "+v"(pl));
+            build_normal(P, mp, pr, pl, cc, bb, eqd);
             to_column(s, cc);  // fresh C0; slacks sp are kept
-            wsync();
             zero_rinv(s);
             wsync();
             rbk = 0;
-            // pstar stays pending (its slack was advanced)
         }
     }
 
