@@ -66,7 +66,10 @@ struct UpdScratch {
 struct QpScratch {
     double L[12][13];       // Cholesky factor of the slot Hessian (row-major, lower)
     double xs[12];          // slot part of x0 = -H^-1 g
+    double ild[12];         // 1 / L_kk
     double ucon[64];
+    double colbuf[NQ];      // column broadcast (equality block)
+    double Rm[12][12];      // equality block: Rm[i][k] = R[k][i]
     union {
         // R^-1 (upper triangular, zero elsewhere): element (i, j) at Rv[j / 2][i].{x, y}[j % 2], so
         // lane i reads its row as 12 conflict-free ds_read_b128 and R^-1 d needs no masking
@@ -195,7 +198,24 @@ __device__ __forceinline__ void quat_R(double qx, double qy, double qz, double q
     R[3] = txy + twz;       R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
     R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
 }
-__device__ __forceinline__ int rp(int i, int j) { return j * (j + 1) / 2 + i; }  // packed upper (i <= j)
+// Reciprocal and reciprocal square root: the hardware estimate (v_rcp_f64 / v_rsq_f64) plus two
+// Newton steps (~1 ulp).  They replace IEEE division / sqrt sequences on the solver's sequential
+// chains (Cholesky pivots, substitutions, Householder scalars), where latency is the cost.
+__device__ __forceinline__ double fast_rcp(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-x, r, 1.0);
+    return fma(r, e, r);
+}
+__device__ __forceinline__ double fast_rsq(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    const double h = 0.5 * x;
+    double e = fma(-h * y, y, 0.5);
+    y = fma(y, e, y);
+    e = fma(-h * y, y, 0.5);
+    return fma(y, e, y);
+}
 __device__ __forceinline__ double sel3(const double* v, int k) { return k == 0 ? v[0] : (k == 1 ? v[1] : v[2]); }
 
 // Diagnostic build only (-DWBC_STAMPS): lane 0 records the shader clock at phase boundaries into
@@ -210,6 +230,30 @@ __device__ __forceinline__ double sel3(const double* v, int k) { return k == 0 ?
     } while (0)
 #else
 #define STAMP(a, rb, slot) do { } while (0)
+#endif
+// Diagnostic build only (-DWBC_ISTAMPS): cycles spent in each sub-step of the active-set loop,
+// summed over its iterations, written to debug slots 0..5 (never read by the kernel).
+#ifdef WBC_ISTAMPS
+#define IST_DECL                                          \
+    unsigned long long ist_prev_ = __builtin_amdgcn_s_memtime(); \
+    unsigned long long ist_acc_[6] = {0, 0, 0, 0, 0, 0}
+#define IST(i)                                                       \
+    do {                                                             \
+        __builtin_amdgcn_sched_barrier(0);                           \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+        ist_acc_[i] += t_ - ist_prev_;                               \
+        ist_prev_ = t_;                                              \
+        __builtin_amdgcn_sched_barrier(0);                           \
+    } while (0)
+#define IST_FLUSH(a, rb)                                                                          \
+    do {                                                                                          \
+        if (lane_id() == 0)                                                                       \
+            for (int i_ = 0; i_ < 6; ++i_) (a).dbg[(size_t)(rb) * WBC_DBG_LEN + i_] = (double)ist_acc_[i_]; \
+    } while (0)
+#else
+#define IST_DECL do { } while (0)
+#define IST(i) do { } while (0)
+#define IST_FLUSH(a, rb) do { } while (0)
 #endif
 
 // ---------------------------------------------------------------------------------------
@@ -857,7 +901,7 @@ __device__ __forceinline__ void to_column(const QpScratch& s, double* cc) {
         double acc = cc[12 + k];
 #pragma unroll
         for (int i = 0; i < k; ++i) acc -= s.L[k][i] * cc[12 + i];
-        cc[12 + k] = acc / s.L[k][k];
+        cc[12 + k] = acc * s.ild[k];
     }
 }
 
@@ -877,34 +921,39 @@ __device__ __forceinline__ void zero_rinv(QpScratch& s) {
 __device__ __forceinline__ double rinv_times_d(const QpScratch& s, const double* d) {
     const int lane = lane_id();
     const int i = lane < NQ ? lane : 0;
-    double acc = 0.0;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};  // independent chains
 #pragma unroll
     for (int jj = 0; jj < NQ / 2; ++jj) {
         const double2 v = s.Rv[jj][i];
-        acc += v.x * d[2 * jj];
-        acc += v.y * d[2 * jj + 1];
+        acc[(2 * jj) & 3] += v.x * d[2 * jj];
+        acc[(2 * jj + 1) & 3] += v.y * d[2 * jj + 1];
     }
-    return lane < NQ ? acc : 0.0;
+    return lane < NQ ? (acc[0] + acc[1]) + (acc[2] + acc[3]) : 0.0;
 }
 // add the constraint with column d at position q: Householder on rows q..23 of every C column
 // (v = d with rows < q zeroed on entry, the Householder vector on exit; dq = d[q]); R^-1 gains the column [-r / alpha; 1 / alpha]
-__device__ __forceinline__ void add_column(QpScratch& s, int q, bool add, double zn, double dq, double rk,
-                                           double* v, double* cc) {
-    const int lane = lane_id();
+__device__ __forceinline__ double householder(int q, bool add, double zn, double dq, double* v, double* cc) {
     if (!add) { zn = 1.0; dq = 0.0; }  // no-op update: vw = 0 below leaves cc bit-identical
-    const double nrm2 = sqrt(zn);
+    const double rs = fast_rsq(zn);
+    const double nrm2 = zn * rs;
     const double alpha = (dq >= 0.0) ? -nrm2 : nrm2;
-    const double beta = 1.0 / (nrm2 * (nrm2 + fabs(dq)));
+    const double ia = (dq >= 0.0) ? -rs : rs;  // 1 / alpha
+    const double beta = fast_rcp(zn + nrm2 * fabs(dq));
     const double vq = dq - alpha;
 #pragma unroll
     for (int k = 0; k < NQ; ++k) v[k] = (k == q) ? vq : v[k];  // in place: d2 -> Householder vector
-    double vw = 0.0;
+    double vp[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int k = 0; k < NQ; ++k) vw += v[k] * cc[k];
-    vw = add ? vw * beta : 0.0;
+    for (int k = 0; k < NQ; ++k) vp[k & 3] += v[k] * cc[k];
+    const double vw = add ? ((vp[0] + vp[1]) + (vp[2] + vp[3])) * beta : 0.0;
 #pragma unroll
     for (int k = 0; k < NQ; ++k) cc[k] -= vw * v[k];
-    const double ia = 1.0 / alpha;
+    return ia;
+}
+__device__ __forceinline__ void add_column(QpScratch& s, int q, bool add, double zn, double dq, double rk,
+                                           double* v, double* cc) {
+    const int lane = lane_id();
+    const double ia = householder(q, add, zn, dq, v, cc);
     if (add && lane <= q) {
         double* col = reinterpret_cast<double*>(&s.Rv[q >> 1][lane]) + (q & 1);
         *col = (lane == q) ? ia : -rk * ia;
@@ -960,12 +1009,14 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
         }
         // right-looking Cholesky, row i in lane i; L_jk broadcast with v_readlane
         bool chol_ok = true;
+        double ildv = 1.0;  // lane k: 1 / L_kk
 #pragma unroll
         for (int k = 0; k < 12; ++k) {
             const double dkk = bcast(hrow[k], k);
             chol_ok &= dkk > 0.0;
-            const double lkk = sqrt(fmax(dkk, 1e-300));
-            const double il = 1.0 / lkk;
+            const double il = fast_rsq(fmax(dkk, 1e-300));
+            const double lkk = dkk * il;
+            if (lane == k) ildv = il;
             hrow[k] = (lane == k) ? lkk : hrow[k] * il;   // L_ik for lanes i > k
 #pragma unroll
             for (int j = k + 1; j < 12; ++j) {
@@ -977,12 +1028,13 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
         if (lane < 12) {
 #pragma unroll
             for (int j = 0; j < 12; ++j) s.L[lane][j] = (j <= lane) ? hrow[j] : 0.0;
+            s.ild[lane] = ildv;
         }
         // forward substitution L z = g_s (column-oriented; z_k from lane k)
         double zk = 0.0;
 #pragma unroll
         for (int k = 0; k < 12; ++k) {
-            const double zz = bcast(gsv / hrow[k], k);  // lane k: g_k' / L_kk
+            const double zz = bcast(gsv * ildv, k);  // lane k: g_k' / L_kk
             if (lane == k) zk = zz;
             if (lane > k) gsv -= hrow[k] * zz;
         }
@@ -994,7 +1046,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
         double zt = zk;
 #pragma unroll
         for (int k = 11; k >= 0; --k) {
-            const double xk = bcast(zt / hrow[k], k);  // lane k: (z_k - sum) / L_kk
+            const double xk = bcast(zt * ildv, k);  // lane k: (z_k - sum) / L_kk
             if (lane == k) s.xs[k] = -xk;              // x0 = -H^-1 g
             if (lane < k) zt -= lcol[k] * xk;
         }
@@ -1003,17 +1055,19 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
 
     STAMP(a, rb, 2);
     double cc[NQ];
-    double bp = 0.0, sp = 0.0, nrm = 1.0;
+    double bp = 0.0, sp = 0.0, nn = 1.0, inrm = 1.0;  // |n_p|^2, 1/|n_p|
     bool is_eq = false, active = false;
     const bool is_con = lane < mp.m;
     {
         build_normal(P, mp, pr, lane, cc, bp, is_eq);
-        double nn = 0.0, sx = 0.0;
+        double np[4] = {0.0, 0.0, 0.0, 0.0}, sq[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int k = 0; k < NQ; ++k) nn += cc[k] * cc[k];
+        for (int k = 0; k < NQ; ++k) np[k & 3] += cc[k] * cc[k];
 #pragma unroll
-        for (int k = 0; k < 12; ++k) sx += cc[12 + k] * s.xs[k];
-        nrm = sqrt(fmax(nn, 1e-300));
+        for (int k = 0; k < 12; ++k) sq[k & 3] += cc[12 + k] * s.xs[k];
+        nn = (np[0] + np[1]) + (np[2] + np[3]);
+        const double sx = (sq[0] + sq[1]) + (sq[2] + sq[3]);
+        inrm = fast_rsq(fmax(nn, 1e-300));
         sp = sx - bp;
         to_column(s, cc);
     }
@@ -1027,12 +1081,138 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
     double u = 0.0;    // multiplier of active slot `lane`
     int act = -1;      // constraint id of active slot `lane`
     int neq_added = 0; // equalities occupy slots 0..neq_added-1
-    int next_eq = 0;
     int pstar = -1;
     int rbk = -1;      // rebuild cursor (>= 0 while re-adding active slot rbk)
     double up = 0.0;
     const double tiny = 1e-26;
     bool done = (status != WBC_QP_OK);
+
+    // Equality block (R1 rows, lanes 0..neq-1).  The dual method adds the
+    // equalities first with full steps; their result is the equality-constrained optimum, which
+    // is computed here in one pass: Householder QR of the equality columns (column broadcast
+    // through LDS), then R^-T v = -s_E, u = R^-1 v and s += C^T [v; 0] in closed form.
+    // Redundant equalities (|d2| ~ 0) are skipped and must be consistent, as in the loop.
+    if (!done && mp.neq > 0) {
+        int myslot = -1;
+        bool redundant = false;
+        int e0 = 0;
+        // fast path, fully unrolled: while no equality has been redundant, equality e goes to slot
+        // q = e, so every row mask below is a compile-time constant
+#pragma unroll
+        for (int e = 0; e < 12; ++e) {
+            if (e < mp.neq && q == e) {
+                if (lane == e) {
+#pragma unroll
+                    for (int k = e & ~1; k < NQ; ++k) s.colbuf[k] = cc[k];
+                }
+                wsync();
+                double d[NQ];
+                double zp[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int k = 0; k < NQ; ++k) {
+                    d[k] = (k >= e) ? s.colbuf[k] : 0.0;
+                    zp[k & 3] += d[k] * d[k];
+                }
+                const double zn = (zp[0] + zp[1]) + (zp[2] + zp[3]);
+                const bool add = !(zn <= tiny * fmax(1.0, bcast(nn, e)));
+                // Householder reflection on rows e..23 (static q = e)
+                {
+                    const double dq = d[e];
+                    const double zs = add ? zn : 1.0, dqs = add ? dq : 0.0;
+                    const double rs = fast_rsq(zs);
+                    const double nrm2 = zs * rs;
+                    const double alpha = (dqs >= 0.0) ? -nrm2 : nrm2;
+                    const double beta = fast_rcp(zs + nrm2 * fabs(dqs));
+                    d[e] = dqs - alpha;
+                    double vp[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                    for (int k = e; k < NQ; ++k) vp[k & 3] += d[k] * cc[k];
+                    const double vw = add ? ((vp[0] + vp[1]) + (vp[2] + vp[3])) * beta : 0.0;
+#pragma unroll
+                    for (int k = e; k < NQ; ++k) cc[k] -= vw * d[k];
+                }
+                if (add) {
+                    if (lane == e) { act = e; myslot = e; }
+                    ++q;
+                } else if (lane == e) {
+                    redundant = true;
+                }
+                e0 = e + 1;
+                wsync();  // colbuf is rewritten next
+            }
+        }
+        // general path (after a redundant equality): dynamic slot q
+#pragma unroll 1
+        for (int e = e0; e < mp.neq; ++e) {
+            if (lane == e) {
+#pragma unroll
+                for (int k = 0; k < NQ; ++k) s.colbuf[k] = cc[k];
+            }
+            wsync();
+            double d[NQ];
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) d[k] = s.colbuf[k];
+            double dq = 0.0, zp[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) {
+                dq = (k == q) ? d[k] : dq;
+                d[k] = (k >= q) ? d[k] : 0.0;
+                zp[k & 3] += d[k] * d[k];
+            }
+            const double zn = (zp[0] + zp[1]) + (zp[2] + zp[3]);
+            const bool add = !(zn <= tiny * fmax(1.0, bcast(nn, e)));
+            householder(q, add, zn, dq, d, cc);
+            if (add) {
+                if (lane == q) act = e;
+                if (lane == e) myslot = q;
+                ++q;
+            } else if (lane == e) {
+                redundant = true;
+            }
+            wsync();  // colbuf is rewritten next
+        }
+        neq_added = q;
+        // R columns and equality slacks by slot
+        if (myslot >= 0) {
+#pragma unroll
+            for (int k = 0; k < 12; ++k) s.Rm[myslot][k] = cc[k];
+            s.colbuf[myslot] = sp;
+        }
+        wsync();
+        // forward substitutions with R^T: v = -R^-T s_E (uniform) and, in lane i, row i of R^-1
+        double v[12], y[12];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+            double av[4] = {0.0, 0.0, 0.0, 0.0}, ay[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int k = 0; k < j; ++k) {
+                const double r = s.Rm[j][k];
+                av[k & 3] += r * v[k];
+                ay[k & 3] += r * y[k];
+            }
+            const bool in = j < q;
+            const double ird = fast_rcp(in ? s.Rm[j][j] : 1.0);
+            const double sj = in ? s.colbuf[j] : 0.0;
+            v[j] = in ? (-sj - ((av[0] + av[1]) + (av[2] + av[3]))) * ird : 0.0;
+            y[j] = in ? (((lane == j) ? 1.0 : 0.0) - ((ay[0] + ay[1]) + (ay[2] + ay[3]))) * ird : 0.0;
+        }
+        double uu[4] = {0.0, 0.0, 0.0, 0.0}, ds[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+            uu[j & 3] += y[j] * v[j];
+            ds[j & 3] += cc[j] * v[j];
+        }
+        if (lane < q) {
+            u = (uu[0] + uu[1]) + (uu[2] + uu[3]);
+#pragma unroll
+            for (int jj = 0; jj < 6; ++jj) s.Rv[jj][lane] = make_double2(y[2 * jj], y[2 * jj + 1]);
+        }
+        sp += (ds[0] + ds[1]) + (ds[2] + ds[3]);
+        const bool bad = redundant && !(fabs(sp) <= 1e-9 * fmax(1.0, fabs(bp)));
+        if (wave_any(bad)) { status = WBC_QP_INFEASIBLE; done = true; }
+        wsync();
+    }
+    IST_DECL;
 
     while (!done) {
         // compiler barrier: LDS reads of the problem (build_normal / to_column on the rare drop
@@ -1040,37 +1220,31 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
         asm volatile("" ::: "memory");
         if (rbk >= q) rbk = -1;  // rebuild finished
         const bool rebuild = rbk >= 0;
-        bool eq_step = false;
         int col, pos;
         if (rebuild) {
             col = bcast_i(act, rbk);
             pos = rbk;
         } else {
-            if (pstar < 0) {
-                if (next_eq < mp.neq) {
-                    pstar = next_eq++;
-                    eq_step = true;
-                } else {
-                    double v = 1e300;
-                    if (is_con && !is_eq && !active) {
-                        const double tol = 1e-10 * fmax(1.0, fabs(bp));
-                        if (sp < -tol) v = sp / nrm;
-                    }
-                    int idx = lane;
-                    wave_argmin(v, idx);
-                    if (!(v < 1e299)) break;  // no violated constraint: optimal
-                    pstar = idx;
+            if (pstar < 0) {  // most violated inequality (equalities are all active already)
+                double v = 1e300;
+                if (is_con && !is_eq && !active) {
+                    const double tol = 1e-10 * fmax(1.0, fabs(bp));
+                    if (sp < -tol) v = sp * inrm;
                 }
+                int idx = lane;
+                wave_argmin(v, idx);
+                if (!(v < 1e299)) break;  // no violated constraint: optimal
+                pstar = idx;
                 up = 0.0;
             }
-            if (!eq_step) {
-                if (++iters > pr.max_wsr) { status = WBC_QP_MAX_ITER; iters = pr.max_wsr; break; }
-            }
+            if (++iters > pr.max_wsr) { status = WBC_QP_MAX_ITER; iters = pr.max_wsr; break; }
             col = pstar;
             pos = q;
         }
+        IST(0);  // selection
         double d[NQ];
         read_column(cc, col, d);
+        IST(1);  // column broadcast
         const double rk = rinv_times_d(s, d);
         double dq = 0.0;
 #pragma unroll
@@ -1078,39 +1252,31 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
             dq = (k == pos) ? d[k] : dq;
             d[k] = (k >= pos) ? d[k] : 0.0;  // d2 (rows >= pos)
         }
-        double cz = 0.0;
+        double czp[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int k = 0; k < NQ; ++k) cz += cc[k] * d[k];  // (C2^T d2)_p = n_p^T z
+        for (int k = 0; k < NQ; ++k) czp[k & 3] += cc[k] * d[k];
+        const double cz = (czp[0] + czp[1]) + (czp[2] + czp[3]);  // (C2^T d2)_p = n_p^T z
         const double zn = bcast(cz, col);                   // |d2|^2: lane col holds d itself
+        IST(2);  // R^-1 d, n^T z, |z|^2
 
         // step (skipped in rebuild mode: the active set is re-added as is)
         bool add = true, drop = false;
         if (!rebuild) {
             const double sps = bcast(sp, pstar);
-            if (eq_step) {
-                const double np2 = bcast(nrm, pstar);
-                if (zn <= tiny * fmax(1.0, np2 * np2)) {
-                    if (!(fabs(sps) <= 1e-9 * fmax(1.0, fabs(bcast(bp, pstar))))) {
-                        status = WBC_QP_INFEASIBLE;
-                        break;
-                    }
-                    add = false;  // redundant, consistent equality: nothing to add
-                }
-            }
-            double t1 = 1e300;
-            int l1 = 64;
-            if (!eq_step) {  // partial step: keep active inequality multipliers >= 0
+            // partial step: keep active inequality multipliers >= 0
+            double t1;
+            int l1 = lane;
+            {
                 double v = 1e300;
-                if (lane < q && lane >= neq_added && rk > 1e-14) v = u / rk;
-                l1 = lane;
+                if (lane < q && lane >= neq_added && rk > 1e-14) v = u * fast_rcp(rk);
                 wave_argmin(v, l1);
                 t1 = v;
             }
-            if (add) {
-                const double t2 = (zn > tiny) ? (-sps / zn) : 1e300;
-                const double t = eq_step ? t2 : fmin(t1, t2);
+            {
+                const double t2 = (zn > tiny) ? (-sps * fast_rcp(zn)) : 1e300;
+                const double t = fmin(t1, t2);
                 if (!(t < 1e299)) { status = WBC_QP_INFEASIBLE; break; }
-                const bool full = eq_step || (t2 < 1e299 && t2 <= t1);
+                const bool full = (t2 < 1e299 && t2 <= t1);
                 if (t2 < 1e299) sp += t * cz;
                 if (lane < q) u -= t * rk;
                 up += t;
@@ -1127,12 +1293,12 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
                     --q;
                     // pstar stays pending (its slack was advanced)
                 }
-            } else {
-                pstar = -1;
             }
         }
+        IST(3);  // step length, multipliers
         // one in-place update site for every path (no second live copy of cc)
         add_column(s, pos, add, zn, dq, rk, d, cc);
+        IST(4);  // Householder update
         if (add) {
             if (rebuild) {
                 ++rbk;
@@ -1140,7 +1306,6 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
                 if (lane == q) { u = up; act = pstar; }
                 if (lane == pstar) active = true;
                 ++q;
-                if (eq_step) neq_added = q;
                 pstar = -1;
             }
             wsync();
@@ -1159,7 +1324,9 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
             wsync();
             rbk = 0;
         }
+        IST(5);  // bookkeeping, barrier, drop path
     }
+    IST_FLUSH(a, rb);
 
     STAMP(a, rb, 4);
     // primal recovery: y = x0 + H^-1 w,  w = sum_k u_k n_{a_k}  (LDS transpose-sum over active rows)
@@ -1181,8 +1348,10 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
     wsync();
     double wi = 0.0;  // w_i for lane i < 24
     if (lane < NQ) {
+        double wp[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int k = 0; k < NQ; ++k) wi += (k < q) ? s.Wt[k][lane] : 0.0;
+        for (int k = 0; k < NQ; ++k) wp[k & 3] += (k < q) ? s.Wt[k][lane] : 0.0;
+        wi = (wp[0] + wp[1]) + (wp[2] + wp[3]);
     }
     // slots: y_s = xs + L^-T L^-1 w_s (lane i < 12 handles row i of the slot block, w_s[i] = w_{12+i})
     double ws = __shfl(wi, (lane + 12) & 63);
@@ -1194,17 +1363,18 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
             lrow[k] = (lane < 12 && k <= lane) ? s.L[lane][k] : 1.0;
             lcol[k] = (lane < 12 && k > lane) ? s.L[k][lane] : 0.0;
         }
+        const double ildv = (lane < 12) ? s.ild[lane] : 1.0;
         double zk = 0.0;
 #pragma unroll
         for (int k = 0; k < 12; ++k) {
-            const double zz = bcast(ws / lrow[k], k);  // lane k: (w_k - sum) / L_kk
+            const double zz = bcast(ws * ildv, k);  // lane k: (w_k - sum) / L_kk
             if (lane == k) zk = zz;
             if (lane > k) ws -= lrow[k] * zz;
         }
         double zt = zk, xk_own = 0.0;
 #pragma unroll
         for (int k = 11; k >= 0; --k) {
-            const double xk = bcast(zt / lrow[k], k);
+            const double xk = bcast(zt * ildv, k);
             if (lane == k) xk_own = xk;
             if (lane < k) zt -= lcol[k] * xk;
         }

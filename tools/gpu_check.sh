@@ -20,6 +20,7 @@ for s in ${STEPS:-smoke pytest bench prof}; do
     pytest) step pytest 600 python -m pytest tests -m gpu -x -q ;;
     bench)  step bench 400 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 ${BENCH_ARGS:-} ;;
     stamps) step stamps 300 env WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_stamps.so python tools/stamps.py stance_cold 4096 ;;
+    istamps) step istamps 300 env WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_istamps.so python tools/istamps.py stance_cold 4096 ;;
     stamps2) step stamps2 300 env WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_stamps.so python tools/stamps.py rl_random 8192 ;;
     variants) step variants 600 python tools/variants.py 30 ;;
     counters) step counters 120 rocprofv3 -L ;;

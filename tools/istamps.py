@@ -1,0 +1,25 @@
+"""Cycles per sub-step of the active-set loop (summed over iterations), from the WBC_ISTAMPS build.
+Usage (GPU box): WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_istamps.so python tools/istamps.py [config] [B]"""
+import json, os, sys
+import numpy as np
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from quadrupedwholebodycontroller_amd import STATELESS, Engine, workloads
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "stance_cold"
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+inp = getattr(workloads, cfg)(B, seed=1)
+e = Engine(B)
+e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
+e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
+for _ in range(3):
+    e.step(STATELESS)
+e.synchronize()
+d = e.debug()[:, 0:6]
+out = e.outputs()
+names = ["selection", "column broadcast", "Rinv d, n^T z, |z|^2", "step/multipliers", "Householder update",
+         "bookkeeping+barrier+drop"]
+it = out["iters"].astype(float)
+res = {n: dict(median=float(np.median(d[:, i])), mean=float(d[:, i].mean())) for i, n in enumerate(names)}
+res["total"] = float(np.median(d.sum(1)))
+res["mean_iters"] = float(it.mean())
+print(json.dumps(dict(config=cfg, batch=B, loop_cycles=res), indent=1))
