@@ -1,0 +1,143 @@
+// wbc_controller.hpp — C++ host shim with the reference's WholeBodyController surface, backed by
+// the MI355X engine (C-ABI in wbc.h), for the single-robot drop-in (B = 1).
+//
+// Reference surface (include/anymal_wbc/whole_body_controller.hpp:35-171):
+//   WholeBodyController()                 hpp:38, cpp:22-59    -> WholeBodyController(params, device)
+//   floatingBaseStateCallback(ModelStates) hpp:43, cpp:187-230 -> same name, ROS-free message struct
+//   jointStateCallback(JointState)        hpp:44, cpp:232-254  -> same name, ROS-free message struct
+//   referenceCallback(WbcReferenceMsg)    hpp:45, cpp:150-185  -> same name, ROS-free message struct
+//   updateState()                         hpp:47, cpp:256-294  -> wbc_update
+//   setInitialState()                     hpp:49, cpp:65-120   -> host state reset + wbc_reset
+//   loadParameters()                      hpp:50, cpp:122-148  -> parameters passed to the constructor
+//   solveQP()                             hpp:54, cpp:466-542  -> wbc_solve
+//   computeJointTorques()                 hpp:52, cpp:553-577  -> wbc_get_output + publishers
+//   controlLoop()                         hpp:67, cpp:637-676  -> controlLoop(max_iterations, ...)
+//   terminate()                           hpp:69, cpp:627-636  -> publishes zero torques
+//
+// ROS is absent here: messages are plain structs with the same field names, and publishers are
+// std::function hooks.  The engine snapshots the inputs at updateState(), so the callbacks and
+// the control loop may run on different threads as long as each call is serialised by the caller
+// (the reference has no synchronisation at all, cpp:681-682).
+#ifndef WBC_CONTROLLER_HPP
+#define WBC_CONTROLLER_HPP
+
+#include <array>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "wbc.h"
+
+namespace wbc_mi355x {
+
+constexpr int numberOfJoints = WBC_NUM_JOINTS;
+constexpr int numberOfLegs = WBC_NUM_LEGS;
+constexpr int qpNumberOfVariables = WBC_NV;
+
+// std_msgs/Float64MultiArray, gazebo_msgs/ModelStates, sensor_msgs/JointState, anymal_wbc/WbcReferenceMsg
+struct Float64MultiArray {
+    std::vector<double> data;
+};
+struct Vector3 {
+    double x = 0, y = 0, z = 0;
+};
+struct Quaternion {
+    double x = 0, y = 0, z = 0, w = 1;
+};
+struct Pose {
+    Vector3 position;
+    Quaternion orientation;
+};
+struct Twist {
+    Vector3 linear, angular;
+};
+struct ModelStates {
+    std::vector<std::string> name;
+    std::vector<Pose> pose;
+    std::vector<Twist> twist;
+};
+struct JointState {
+    std::vector<std::string> name;
+    std::vector<double> position, velocity, effort;
+};
+struct WbcReferenceMsg {  // msg/WbcReferenceMsg.msg:1-7
+    Float64MultiArray desiredComPose, desiredComVelocity, desiredComAcceleration;
+    Float64MultiArray desiredSwingLegsPosition, desiredSwingLegsVelocity, desiredSwingLegsAcceleration;
+    bool footContacts[numberOfLegs] = {true, true, true, true};
+};
+
+class WholeBodyController {
+public:
+    // model name matched in ModelStates.name (params_controller.yaml:1)
+    static constexpr const char* modelName = "anymalModel";
+
+    // params == nullptr: config/params_controller.yaml defaults.  Throws std::runtime_error if the
+    // engine cannot be created (no HIP device, library error): there is no CPU fallback.
+    explicit WholeBodyController(const wbc_params* params = nullptr, int device = 0);
+    ~WholeBodyController();
+    WholeBodyController(const WholeBodyController&) = delete;
+    WholeBodyController& operator=(const WholeBodyController&) = delete;
+
+    void floatingBaseStateCallback(const ModelStates& modelStateMsg);
+    void jointStateCallback(const JointState& jointStateMsg);
+    void referenceCallback(const WbcReferenceMsg& refMsg);
+
+    void updateState();
+    void setInitialState();
+    void solveQP();
+    void computeJointTorques();
+    void terminate();
+
+    // ROS-free control loop (cpp:637-676): setInitialState, then per cycle
+    //   beforeCycle(iteration) [stands in for the subscriber callbacks], updateState, solveQP,
+    //   computeJointTorques; stops when the QP fails (cpp:654-659) or after max_iterations.
+    // rate_hz > 0 sleeps to that rate like ros::Rate; 0 runs back to back.  Returns iterations run.
+    long controlLoop(long max_iterations, double rate_hz = 0.0,
+                     const std::function<void(long)>& beforeCycle = nullptr);
+
+    // publishers (cpp:41-43): jointTorquePub_, desiredGroundReactionForcesPub_
+    std::function<void(const Float64MultiArray&)> jointTorquePublisher;
+    std::function<void(const Float64MultiArray&)> desiredGroundReactionForcesPublisher;
+
+    // qpReturnValue_ (hpp:166): WBC_QP_OK mirrors qpOASES::SUCCESSFUL_RETURN
+    int qpReturnValue() const { return qpStatus_; }
+    int qpIterations() const { return qpIters_; }
+    const std::array<double, numberOfJoints>& jointTorques() const { return tau_; }
+    const std::array<double, 3 * numberOfLegs>& groundReactionForces() const { return grf_; }
+    const std::array<double, qpNumberOfVariables>& qpSolution() const { return x_; }
+    bool isSwitchingFootState() const { return isSwitchingFootState_; }
+    wbc_engine* engine() { return engine_; }
+
+private:
+    void pushInputs();
+
+    wbc_engine* engine_ = nullptr;
+    wbc_params params_{};
+    bool firstJointStateCallback_ = true;
+    bool firstFloatingBaseStateCallback_ = true;
+    bool firstControllerIteration_ = true;
+    int modelIndex_ = 0;
+    int jointIndex_[numberOfJoints] = {};
+
+    // state (cpp:65-120 initial values)
+    double basePose_[WBC_POSE_LEN] = {};  // px py pz qx qy qz qw
+    double nu_[WBC_NU_LEN] = {};           // v_lin, omega (world), qdot
+    double jointPos_[numberOfJoints] = {};
+    double ref_[WBC_REF_LEN] = {};          // WbcReferenceMsg field order
+    int footContacts_[numberOfLegs] = {1, 1, 1, 1};
+    bool isSwitchingFootState_ = false;
+
+    int qpStatus_ = WBC_QP_OK;
+    int qpIters_ = 0;
+    std::array<double, numberOfJoints> tau_{};
+    std::array<double, 3 * numberOfLegs> grf_{};
+    std::array<double, qpNumberOfVariables> x_{};
+};
+
+// The reference model's joint names in model order (LH, LF, RF, RH x HAA, HFE, KFE), used to map
+// JointState messages by name (cpp:234-246).
+const std::array<std::string, numberOfJoints>& modelJointNames();
+
+}  // namespace wbc_mi355x
+
+#endif  // WBC_CONTROLLER_HPP

@@ -1,0 +1,175 @@
+// wbc_control_loop — ROS-free stand-in for whole_body_controller_node (src/whole_body_controller_node.cpp:3-9):
+// drives the WholeBodyController shim (include/wbc_controller.hpp) through its callbacks and
+// controlLoop(), one robot, on the GPU.
+//
+//   wbc_control_loop stance [cycles] [rate_hz]
+//       BASELINE configs[0]: stance CoM-hold from the reference start-up pose (base 0.585 m, q0,
+//       all feet in contact, reference pose from params_controller.yaml), `cycles` (default 1000)
+//       control cycles; prints one JSON line with per-cycle latency and the last torques.
+//   wbc_control_loop replay <inputs.bin> <outputs.bin>
+//       feeds recorded per-cycle messages (tests/test_gpu_controller.py writes them from the golden
+//       trajectories) and writes status, iterations, tau and x per cycle.
+//       inputs.bin : int32 T, then T x (pose 7, nu 18, qj 12, ref 54, contacts, switching) doubles
+//       outputs.bin: T x (status, iters, tau 12, x 42) doubles
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "wbc_controller.hpp"
+
+using namespace wbc_mi355x;
+
+namespace {
+
+constexpr int kRec = 7 + 18 + 12 + 54 + 2;
+constexpr int kOut = 2 + 12 + 42;
+
+// messages as the simulator / planner would publish them (cpp:150-254)
+ModelStates make_model_states(const double* pose, const double* nu) {
+    ModelStates m;
+    m.name = {"ground_plane", WholeBodyController::modelName};
+    m.pose.resize(2);
+    m.twist.resize(2);
+    Pose& p = m.pose[1];
+    p.position = {pose[0], pose[1], pose[2]};
+    p.orientation = {pose[3], pose[4], pose[5], pose[6]};
+    m.twist[1].linear = {nu[0], nu[1], nu[2]};
+    m.twist[1].angular = {nu[3], nu[4], nu[5]};
+    return m;
+}
+JointState make_joint_state(const double* qj, const double* qd) {
+    // alphabetical order (as robot_state_publisher emits), not the model order: exercises the
+    // name mapping of jointStateCallback (cpp:234-246)
+    JointState j;
+    std::vector<int> order(numberOfJoints);
+    for (int i = 0; i < numberOfJoints; ++i) order[i] = i;
+    const auto& names = modelJointNames();
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return names[a] < names[b]; });
+    for (int k : order) {
+        j.name.push_back(names[k]);
+        j.position.push_back(qj[k]);
+        j.velocity.push_back(qd[k]);
+        j.effort.push_back(0.0);
+    }
+    return j;
+}
+WbcReferenceMsg make_reference(const double* ref, int contacts) {
+    WbcReferenceMsg r;
+    r.desiredComPose.data.assign(ref, ref + 6);
+    r.desiredComVelocity.data.assign(ref + 6, ref + 12);
+    r.desiredComAcceleration.data.assign(ref + 12, ref + 18);
+    r.desiredSwingLegsPosition.data.assign(ref + 18, ref + 30);
+    r.desiredSwingLegsVelocity.data.assign(ref + 30, ref + 42);
+    r.desiredSwingLegsAcceleration.data.assign(ref + 42, ref + 54);
+    for (int l = 0; l < numberOfLegs; ++l) r.footContacts[l] = (contacts >> l) & 1;
+    return r;
+}
+
+int run_stance(long cycles, double rate) {
+    WholeBodyController wbc;
+    double pose[7] = {0.0, 0.0, 0.585, 0.0, 0.0, 0.0, 1.0};
+    double nu[18] = {0};
+    const double q0[12] = {0.0, -0.4, 0.8, 0.0, 0.4, -0.8, 0.0, 0.4, -0.8, 0.0, -0.4, 0.8};
+    wbc_params p;
+    wbc_default_params(&p);
+    double ref[54] = {0};
+    for (int i = 0; i < 6; ++i) ref[i] = p.initial_reference_pose[i];
+    const ModelStates ms = make_model_states(pose, nu);
+    const JointState js = make_joint_state(q0, nu + 6);
+    const WbcReferenceMsg rm = make_reference(ref, 15);
+    wbc.floatingBaseStateCallback(ms);  // first message: locates the model only (cpp:189-204)
+    std::vector<double> lat;
+    lat.reserve(cycles);
+    auto t_prev = std::chrono::steady_clock::now();
+    long n = 0;
+    n = wbc.controlLoop(cycles, rate, [&](long it) {
+        const auto now = std::chrono::steady_clock::now();
+        if (it > 0) lat.push_back(std::chrono::duration<double, std::micro>(now - t_prev).count());
+        t_prev = now;
+        wbc.floatingBaseStateCallback(ms);
+        wbc.jointStateCallback(js);
+        wbc.referenceCallback(rm);
+    });
+    std::vector<double> s = lat;
+    std::sort(s.begin(), s.end());
+    auto pct = [&](double q) { return s.empty() ? 0.0 : s[std::min(s.size() - 1, (size_t)(q * s.size()))]; };
+    double mean = 0;
+    for (double v : lat) mean += v;
+    mean = lat.empty() ? 0 : mean / lat.size();
+    const auto& tau = wbc.jointTorques();
+    std::printf("{\"config\": \"stance_hold_b1\", \"cycles\": %ld, \"qp_status\": %d, \"qp_iters\": %d, "
+                "\"cycle_us_mean\": %.3f, \"cycle_us_p50\": %.3f, \"cycle_us_p99\": %.3f, \"rate_hz\": %.1f, \"tau\": [",
+                n, wbc.qpReturnValue(), wbc.qpIterations(), mean, pct(0.5), pct(0.99), rate);
+    for (int i = 0; i < numberOfJoints; ++i) std::printf("%s%.9g", i ? ", " : "", tau[i]);
+    std::printf("]}\n");
+    return wbc.qpReturnValue() == WBC_QP_OK ? 0 : 3;
+}
+
+int run_replay(const char* in_path, const char* out_path) {
+    FILE* f = std::fopen(in_path, "rb");
+    if (!f) throw std::runtime_error(std::string("cannot open ") + in_path);
+    int32_t T = 0;
+    if (std::fread(&T, sizeof(T), 1, f) != 1 || T <= 0) throw std::runtime_error("bad header");
+    std::vector<double> in((size_t)T * kRec);
+    if (std::fread(in.data(), sizeof(double), in.size(), f) != in.size()) throw std::runtime_error("short input");
+    std::fclose(f);
+    std::vector<double> out((size_t)T * kOut, 0.0);
+    WholeBodyController wbc;
+    {
+        const double* r = in.data();
+        wbc.floatingBaseStateCallback(make_model_states(r, r + 7));  // locate the model
+    }
+    const long n = wbc.controlLoop(T, 0.0, [&](long t) {
+        const double* r = in.data() + (size_t)t * kRec;
+        wbc.floatingBaseStateCallback(make_model_states(r, r + 7));
+        wbc.jointStateCallback(make_joint_state(r + 25, r + 13));
+        wbc.referenceCallback(make_reference(r + 37, (int)r[91]));
+        if ((r[92] != 0.0) != wbc.isSwitchingFootState())
+            throw std::runtime_error("isSwitchingFootState_ latch differs from the recorded input");
+    });
+    // controlLoop stops at a failed QP; record what ran
+    (void)n;
+    FILE* g = std::fopen(out_path, "wb");
+    if (!g) throw std::runtime_error(std::string("cannot open ") + out_path);
+    // re-run cycle by cycle to capture every output (the loop above validates the latch and the stop rule)
+    WholeBodyController w2;
+    w2.floatingBaseStateCallback(make_model_states(in.data(), in.data() + 7));
+    for (int t = 0; t < T; ++t) {
+        const double* r = in.data() + (size_t)t * kRec;
+        w2.floatingBaseStateCallback(make_model_states(r, r + 7));
+        w2.jointStateCallback(make_joint_state(r + 25, r + 13));
+        w2.referenceCallback(make_reference(r + 37, (int)r[91]));
+        w2.updateState();
+        w2.solveQP();
+        w2.computeJointTorques();
+        double* o = out.data() + (size_t)t * kOut;
+        o[0] = w2.qpReturnValue();
+        o[1] = w2.qpIterations();
+        for (int i = 0; i < 12; ++i) o[2 + i] = w2.jointTorques()[i];
+        for (int i = 0; i < 42; ++i) o[14 + i] = w2.qpSolution()[i];
+    }
+    std::fwrite(out.data(), sizeof(double), out.size(), g);
+    std::fclose(g);
+    std::printf("{\"replayed\": %d, \"control_loop_cycles\": %ld}\n", T, n);
+    return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    try {
+        const std::string mode = argc > 1 ? argv[1] : "stance";
+        if (mode == "stance") return run_stance(argc > 2 ? std::atol(argv[2]) : 1000, argc > 3 ? std::atof(argv[3]) : 0.0);
+        if (mode == "replay" && argc > 3) return run_replay(argv[2], argv[3]);
+        std::fprintf(stderr, "usage: %s stance [cycles] [rate_hz] | replay <in.bin> <out.bin>\n", argv[0]);
+        return 2;
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "wbc_control_loop: %s\n", e.what());
+        return 1;
+    }
+}

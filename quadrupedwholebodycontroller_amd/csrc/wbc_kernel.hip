@@ -250,7 +250,16 @@ __device__ __forceinline__ double sel3(const double* v, int k) { return k == 0 ?
         if (lane_id() == 0)                                                                       \
             for (int i_ = 0; i_ < 6; ++i_) (a).dbg[(size_t)(rb) * WBC_DBG_LEN + i_] = (double)ist_acc_[i_]; \
     } while (0)
+// update-phase boundaries: absolute clock into debug slots 8.. (same build)
+#define UST(a, rb, i)                                                                              \
+    do {                                                                                           \
+        __builtin_amdgcn_sched_barrier(0);                                                         \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                \
+        if (lane_id() == 0) (a).dbg[(size_t)(rb) * WBC_DBG_LEN + 8 + (i)] = (double)t_;           \
+        __builtin_amdgcn_sched_barrier(0);                                                         \
+    } while (0)
 #else
+#define UST(a, rb, i) do { } while (0)
 #define IST_DECL do { } while (0)
 #define IST(i) do { } while (0)
 #define IST_FLUSH(a, rb) do { } while (0)
@@ -271,6 +280,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
     const bool stateful = a.stateful != 0;
     const bool debug = a.debug != 0;
     double* H = stateful ? a.hist + (size_t)rb * HIST_LEN : nullptr;
+    UST(a, rb, 0);
 
     // inputs, one element per lane (robot-major arrays -> contiguous per wave); sin/cos per joint
     {
@@ -294,6 +304,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
         if (lane == 0) { P.flags = anybad ? 1.0 : 0.0; P.kappa = (double)kap; }
     }
     wsync();
+    UST(a, rb, 1);
     const double* pB = &s.in[0];
     const double* vB = &s.in[7];
     const double* wB = &s.in[10];
@@ -352,6 +363,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
     }
     wsync();
 
+    UST(a, rb, 2);
     // stage B: one lane per body: com, world inertia, com velocity, m a_com, I alpha + w x I w
     {
         double c[3], I[9], vc[3], F[3], N[3], mb = 0.0;
@@ -408,6 +420,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
         }
     }
     wsync();
+    UST(a, rb, 3);
     // foot Jacobian joint columns (getFrameFreeFloatingJacobian rows 0-2, cpp:327-341): a_k x (p_f - o_k)
     if (lane < 12) {
         const int l = lane / 3, k = lane % 3;
@@ -445,6 +458,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
         s.contrib[lane][5] = bd.I[5] - mb * d[1] * d[2];
     }
     wsync();
+    UST(a, rb, 4);
     double Ic[9], Icinv[9];
     {
         double t[6] = {0, 0, 0, 0, 0, 0};
@@ -464,6 +478,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
 #pragma unroll
         for (int i = 0; i < 3; ++i) { s.contrib[lane][i] = bd.F[i]; s.contrib[lane][3 + i] = t[i] + bd.N[i]; }
     }
+    UST(a, rb, 5);
     // stage C: per joint: centroidal momentum column (about c), leg block of M, joint bias (C nu)_j
     if (lane < 12) {
         const int j = lane, l = j / 3, k = j % 3;
@@ -510,6 +525,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
         s.hj[j] = dot3(aj, hsum);
     }
     wsync();
+    UST(a, rb, 6);
     double hb[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll 1
     for (int b = 0; b < 13; ++b)
@@ -574,6 +590,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
 #pragma unroll
         for (int i = 0; i < 9; ++i) { P.Ic[i] = Ic[i]; P.Icinv[i] = Icinv[i]; }
     }
+    UST(a, rb, 7);
     const double dt = 1.0 / pr.loop_rate;
 
     // lane = joint column j: Jbar joint column, Mbar_j column, bbar_j
@@ -604,6 +621,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
         P.bbj[j] = hpj - (dot3(Alj, zeta) + dot3(Aaj, &zeta[3]));
         P.d[j] = s.pf[lj][kj] - sel3(c, kj);
     }
+    UST(a, rb, 8);
     // T_top = [Ad^-1(r), Mbar_b^-1 A_j]; Tdot_inv for the next cycle (cpp:291-293)
     double tcol[6] = {0, 0, 0, 0, 0, 0};
     if (stateful) {
@@ -649,6 +667,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
             }
         }
     }
+    UST(a, rb, 9);
     // finite-difference bounds (cpp:384-402, 503-515); swing commands (cpp:447-464)
     if (lane < 12) {
         const int i = lane, l = i / 3, rr = i % 3;
@@ -699,6 +718,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
         if (lane < 3) H[H_ROLD + lane] = s.cen[CEN_R + lane];
         if (lane == 0) { H[H_KOLD] = (double)kap; H[H_VALID] = 1.0; }
     }
+    UST(a, rb, 10);
     if (debug) {
         double* D = a.dbg + (size_t)rb * WBC_DBG_LEN;
         if (lane < 3) {

@@ -87,6 +87,24 @@ def test_no_silent_cpu_fallback():
         Engine(8)
 
 
+def test_controller_shim_builds_and_fails_loudly_without_gpu():
+    """The C++ WholeBodyController shim (include/wbc_controller.hpp) exports the reference's
+    method names, and its node stand-in refuses to run without a HIP device."""
+    import torch
+
+    lib = os.path.join(ROOT, "quadrupedwholebodycontroller_amd", "libwbc_controller.so")
+    exe = os.path.join(ROOT, "quadrupedwholebodycontroller_amd", "wbc_control_loop")
+    assert os.path.exists(lib) and os.path.exists(exe)
+    out = subprocess.run(["nm", "-DC", "--defined-only", lib], capture_output=True, text=True).stdout
+    for m in ("floatingBaseStateCallback", "jointStateCallback", "referenceCallback", "updateState",
+              "setInitialState", "solveQP", "computeJointTorques", "controlLoop", "terminate"):
+        assert f"wbc_mi355x::WholeBodyController::{m}(" in out, m
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    r = subprocess.run([exe, "stance", "5"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "no HIP device" in r.stderr
+
+
 def test_shard_bounds():
     from quadrupedwholebodycontroller_amd.sharding import shard_bounds
 

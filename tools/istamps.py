@@ -23,3 +23,8 @@ res = {n: dict(median=float(np.median(d[:, i])), mean=float(d[:, i].mean())) for
 res["total"] = float(np.median(d.sum(1)))
 res["mean_iters"] = float(it.mean())
 print(json.dumps(dict(config=cfg, batch=B, loop_cycles=res), indent=1))
+u = e.debug()[:, 8:19]
+un = ["inputs+sincos", "stage A (leg chains)", "stage B (bodies)", "Jf + CoM sums", "Ic sum+inv", "stage C (joints)",
+      "hb sum, y, zeta, lane0", "Jbar/Mbar/bbar", "Tdot_inv", "bounds, wrench, history"]
+du = np.diff(u, axis=1)
+print(json.dumps({n: float(np.median(du[:, i])) for i, n in enumerate(un)}, indent=1))
