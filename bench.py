@@ -79,11 +79,31 @@ def cpu_baseline(inp, budget_s=15.0):
                 sample=f"{n} cold solves through oracle/wbc_np.py (numpy restatement), 1 thread, {dt:.2f} s")
 
 
+def committed_traffic(workload, batch):
+    """HBM bytes per launch of wbc_step_kernel from a committed PMC summary (tools/pmc_summary.py)
+    taken on this exact kernel source, workload and batch; None if there is none."""
+    import glob
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from pmc_summary import kernel_source_hash
+
+    want = kernel_source_hash()
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_*.json")), reverse=True):
+        try:
+            rec = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if (rec.get("kernel_source_sha256") == want and rec.get("workload") == workload and
+                rec.get("batch") == batch and "traffic_bytes_per_launch" in rec):
+            return rec["traffic_bytes_per_launch"], os.path.relpath(f, ROOT)
+    return None, None
+
+
 def bench_trot(torch, stream, device, STATELESS, B=4096, T=400, seed=2):
     """BASELINE configs[2]: B robots trotting for T cycles (1 s at 400 Hz), alternating 2-contact
     modes, history carried across steps (stateful path: finite differences, Tdot_inv lag, integral
     error).  All T steps of inputs are staged in HBM first and bound per step (no copies timed)."""
-    from quadrupedwholebodycontroller_amd import Engine, workloads
+    from quadrupedwholebodycontroller_amd import NO_X, Engine, workloads
 
     seq = list(workloads.trot_sequence(B, steps=T, seed=seed))
     dev = {k: torch.from_numpy(np.ascontiguousarray(np.stack([s[k] for s in seq]))).to(f"cuda:{device}")
@@ -97,7 +117,7 @@ def bench_trot(torch, stream, device, STATELESS, B=4096, T=400, seed=2):
             e.bind_device_inputs(dev["base_pose"][t].data_ptr(), dev["nu"][t].data_ptr(), dev["qj"][t].data_ptr(),
                                  dev["ref"][t].data_ptr(), dev["contacts"][t].data_ptr(),
                                  dev["switching"][t].data_ptr())
-            e.step(0)
+            e.step(NO_X)  # stateful
 
     run()  # warm-up pass
     torch.cuda.synchronize()
@@ -144,7 +164,9 @@ def main():
     else:
         torch.cuda.set_device(local_rank)
 
-    from quadrupedwholebodycontroller_amd import STATELESS, Engine, workloads
+    from quadrupedwholebodycontroller_amd import NO_X, STATELESS, Engine, workloads
+
+    STEP_FLAGS = STATELESS | NO_X  # cold solves; outputs tau, grf, status, iters (the published ones)
 
     cfg = CONFIGS[args.config]
     B = args.batch or cfg["batch"]
@@ -164,7 +186,7 @@ def main():
     tau_all = torch.zeros(world * B * 12, dtype=torch.float64, device="cuda") if world > 1 else None
 
     def one_step():
-        e.step(STATELESS)
+        e.step(STEP_FLAGS)
         if world > 1:
             dist.all_gather_into_tensor(tau_all, tau_local)
 
@@ -191,7 +213,7 @@ def main():
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record(stream)
     for _ in range(args.steps):
-        e.step(STATELESS)
+        e.step(STEP_FLAGS)
     ev1.record(stream)
     torch.cuda.synchronize()
     kernel_ms = ev0.elapsed_time(ev1) / args.steps
@@ -245,6 +267,7 @@ def main():
                                mean_iters=float(o2["iters"].mean()), desc=c2["desc"])
             e2.close()
 
+    traffic, traffic_src = committed_traffic(args.config, B)
     total = B * world * args.steps
     value = total / elapsed
     result = {
@@ -264,12 +287,12 @@ def main():
                    "global_batch": B * world, "parallelism": f"dp{world} (robot shards) + RCCL all-gather of tau"
                    if world > 1 else "dp1"},
         "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": None,
+                     "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "wbc_step_kernel", "kernel_ms": kernel_ms,
                      "note": "fp64 compute roof (gfx950 fp64 vector = matrix peak); algorithmic flops F(k) of "
                              "SURVEY 8(d), k = iters[] per robot; the path is latency-bound, not HBM-bound"},
         "roofline_hbm": {"bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": hbm_gbs / HBM_PEAK_GBS, "bytes_per_solve": BYTES_COLD},
+                         "frac": hbm_gbs / HBM_PEAK_GBS, "bytes_per_solve": BYTES_COLD, "traffic": traffic},
         "qp_status_counts": np.bincount(status, minlength=4).tolist(),
         "mean_iters": float(iters.mean()),
     }

@@ -105,6 +105,7 @@ enum {
 /* Step flags. */
 #define WBC_STATELESS 1u /* cold step: history = reset values; history is neither read nor written */
 #define WBC_DEBUG 2u     /* also write the per-robot debug record (wbc_get_debug) */
+#define WBC_NO_X 4u      /* skip the x[42] output (tau, grf, status, iters are still written) */
 
 /* Debug record layout (doubles per robot), written by update/step under WBC_DEBUG. */
 enum {

@@ -94,7 +94,7 @@ wbc::KernelArgs make_args(wbc_engine* h, uint32_t flags) {
     a.work = h->d_work;
     a.tau = h->out_tau;
     a.grf = h->out_grf;
-    a.x = h->out_x;
+    a.x = (flags & WBC_NO_X) ? nullptr : h->out_x;
     a.status = h->out_status;
     a.iters = h->out_iters;
     a.dbg = h->d_dbg;

@@ -173,3 +173,21 @@ def test_device_bound_inputs_and_outputs():
     assert np.array_equal(grf.cpu().numpy(), host["grf"])
     assert np.array_equal(status.cpu().numpy(), host["status"])
     e.close()
+
+
+def test_no_x_flag_keeps_published_outputs():
+    """WBC_NO_X skips only the x[42] row; tau, grf, status, iters are bit-identical."""
+    from quadrupedwholebodycontroller_amd import NO_X
+
+    B = 200
+    inp = workloads.rl_random(B, seed=51)
+    e = Engine(B)
+    e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
+    e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
+    e.step(STATELESS)
+    full = e.outputs()
+    e.step(STATELESS | NO_X)
+    lean = e.outputs()
+    e.close()
+    for k in ("tau", "grf", "status", "iters"):
+        assert np.array_equal(full[k], lean[k]), k

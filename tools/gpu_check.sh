@@ -22,7 +22,7 @@ for s in ${STEPS:-smoke pytest bench prof}; do
     stamps) step stamps 300 env WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_stamps.so python tools/stamps.py stance_cold 4096 ;;
     istamps) step istamps 300 env WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_istamps.so python tools/istamps.py stance_cold 4096 ;;
     stamps2) step stamps2 300 env WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_stamps.so python tools/stamps.py rl_random 8192 ;;
-    variants) step variants 600 python tools/variants.py 30 ;;
+    variants) step variants 600 python tools/variants.py 30 ${VARIANTS:-w2,w3,w4,w5} ;;
     counters) step counters 120 rocprofv3 -L ;;
     pmc)    step pmc 1200 bash tools/pmc.sh ;;
     prof)   step prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o $TAG --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;

@@ -16,6 +16,17 @@ import os
 import sys
 
 
+def kernel_source_hash():
+    """Hash of the HIP source the counters were taken on (bench.py only uses a matching record)."""
+    import hashlib
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    h = hashlib.sha256()
+    for f in ("wbc_kernel.hip", "wbc_layout.h"):
+        h.update(open(os.path.join(root, "quadrupedwholebodycontroller_amd", "csrc", f), "rb").read())
+    return h.hexdigest()
+
+
 def summarise(pmc_dir, kernel="wbc_step_kernel"):
     vals = collections.defaultdict(list)
     for f in sorted(glob.glob(os.path.join(pmc_dir, "pass*_counter_collection.csv"))):
@@ -31,7 +42,8 @@ def main():
     workload = sys.argv[4] if len(sys.argv) > 4 else "stance_cold_b4096"
     batch = int(sys.argv[5]) if len(sys.argv) > 5 else 4096
     mean, n = summarise(pmc_dir, kernel)
-    rec = {"kernel": kernel, "workload": workload, "batch": batch, "dispatches": n, "per_launch": mean}
+    rec = {"kernel": kernel, "workload": workload, "batch": batch, "dispatches": n, "per_launch": mean,
+           "kernel_source_sha256": kernel_source_hash()}
     if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
         rd = 2.0 * mean["FETCH_SIZE"] * 1024.0
         wr = mean["WRITE_SIZE"] * 1024.0

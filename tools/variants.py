@@ -28,9 +28,12 @@ for name, gen, B in (("stance_cold_b4096", workloads.stance_cold, 4096), ("rl_ra
 print(json.dumps(res))
 ''' % ROOT
 steps = sys.argv[1] if len(sys.argv) > 1 else "30"
+names = sys.argv[2].split(",") if len(sys.argv) > 2 else ["w2", "w3", "w4", "w5"]
 out = {}
-for w in (2, 3, 4, 5):
-    lib = os.path.join(ROOT, "quadrupedwholebodycontroller_amd", f"libwbc_hip_w{w}.so")
-    r = subprocess.run([sys.executable, "-c", CHILD, steps], env=dict(os.environ, WBC_LIB=lib), capture_output=True, text=True, timeout=300)
-    out[f"w{w}"] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else dict(error=r.stderr[-500:])
-    print(f"w{w}", json.dumps(out[f"w{w}"]), flush=True)
+for rep in range(2):  # two passes, interleaved, to expose box-to-box / run-to-run drift
+    for n in names:
+        lib = os.path.join(ROOT, "quadrupedwholebodycontroller_amd", f"libwbc_hip_{n}.so")
+        r = subprocess.run([sys.executable, "-c", CHILD, steps], env=dict(os.environ, WBC_LIB=lib), capture_output=True,
+                           text=True, timeout=300)
+        res = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else dict(error=r.stderr[-500:])
+        print(f"{n}#{rep}", json.dumps(res), flush=True)
