@@ -209,7 +209,9 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
-    # kernel-only timing with HIP events on the launch stream (for the roofline)
+    # kernel duration for the roofline: HIP events on the launch stream around K back-to-back
+    # launches of the step kernel (the engine's only kernel per step).  This includes the few-us
+    # dispatch gap between launches; rocprofv3's per-dispatch average (profiles/) excludes it.
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record(stream)
     for _ in range(args.steps):

@@ -781,7 +781,13 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
             }
             D[WBC_DBG_M + e] = v;
         }
-        if (lane < 18) D[WBC_DBG_CNU + lane] = (lane < 6) ? sel3(lane < 3 ? hb : &hb[3], lane % 3) : s.hj[lane - 6];
+        if (lane < 18) {
+            // register selects (a pointer select into hb[] would put hb in scratch memory)
+            double v6 = hb[0];
+#pragma unroll
+            for (int k = 1; k < 6; ++k) v6 = (lane == k) ? hb[k] : v6;
+            D[WBC_DBG_CNU + lane] = (lane < 6) ? v6 : s.hj[lane - 6];
+        }
         for (int e = lane; e < 216; e += 64) {
             const int i = e / 18, j = e % 18, l = i / 3, rr = i % 3;
             double v, vb;
