@@ -31,6 +31,8 @@ CONFIGS = {
                               desc="BASELINE configs[1]: B=4096 4-contact stance QPs, fp64, cold start"),
     "rl_random_b8192": dict(gen="rl_random", batch=8192, seed=3,
                             desc="BASELINE configs[3] per-GPU shard: randomized q/qd, 16 contact masks, cold"),
+    "modes16_b16384": dict(gen="modes16", batch=16384, seed=4,
+                           desc="BASELINE configs[4] per-GPU shard: 1024 states x all 16 contact masks, cold"),
 }
 
 
@@ -256,10 +258,10 @@ def main():
             e2.set_state(inp2["base_pose"], inp2["nu"], inp2["qj"])
             e2.set_reference(inp2["ref"], inp2["contacts"], inp2["switching"])
             for _ in range(args.warmup):
-                e2.step(STATELESS)
+                e2.step(STEP_FLAGS)
             ev0.record(stream)
             for _ in range(args.steps):
-                e2.step(STATELESS)
+                e2.step(STEP_FLAGS)
             ev1.record(stream)
             torch.cuda.synchronize()
             ms2 = ev0.elapsed_time(ev1) / args.steps

@@ -68,6 +68,11 @@ def mode_hypotheses(n_states=8192, seed=4):
     return rep
 
 
+def modes16(B=16384, seed=4):
+    """Config 5 shard of B QPs: B // 16 states, each under all 16 contact masks."""
+    return mode_hypotheses(B // 16, seed)
+
+
 TROT_PERIOD_STEPS = 100  # 0.25 s at 400 Hz per half-cycle
 
 
