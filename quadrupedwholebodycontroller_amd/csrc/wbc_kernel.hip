@@ -274,8 +274,10 @@ __device__ __forceinline__ double sel3(const double* v, int k) { return k == 0 ?
         if (lane_id() == 0) (a).dbg[(size_t)(rb) * WBC_DBG_LEN + 8 + (i)] = (double)t_;           \
         __builtin_amdgcn_sched_barrier(0);                                                         \
     } while (0)
+#define EST(a, rb, i) UST(a, rb, 12 + (i))  // equality block / solve setup boundaries: slots 20..
 #else
 #define UST(a, rb, i) do { } while (0)
+#define EST(a, rb, i) do { } while (0)
 #define IST_DECL do { } while (0)
 #define IST(i) do { } while (0)
 #define IST_FLUSH(a, rb) do { } while (0)
@@ -300,21 +302,23 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
 
     // inputs, one element per lane (robot-major arrays -> contiguous per wave); sin/cos per joint
     {
-        bool bad = false;
-        for (int k = lane; k < 91; k += 64) {
-            double v;
-            if (k < 7) v = a.base_pose[(size_t)rb * 7 + k];
-            else if (k < 25) v = a.nu[(size_t)rb * 18 + (k - 7)];
-            else if (k < 37) v = a.qj[(size_t)rb * 12 + (k - 25)];
-            else v = a.ref[(size_t)rb * 54 + (k - 37)];
-            bad |= !isfinite(v);
-            s.in[k] = v;
-        }
-        if (lane < 12) {
+        // both loads issued before either is used: lane k < 64 reads input k, lanes 0..26 also
+        // read input 64 + k (all in the reference block)
+        const double* p0 = (lane < 7) ? a.base_pose + (size_t)rb * 7 + lane
+                         : (lane < 25) ? a.nu + (size_t)rb * 18 + (lane - 7)
+                         : (lane < 37) ? a.qj + (size_t)rb * 12 + (lane - 25)
+                                       : a.ref + (size_t)rb * 54 + (lane - 37);
+        const bool two = lane + 64 < 91;
+        const double v0 = *p0;
+        const double v1 = two ? a.ref[(size_t)rb * 54 + (lane + 64 - 37)] : 0.0;
+        const bool bad = !isfinite(v0) || !isfinite(v1);
+        s.in[lane] = v0;
+        if (two) s.in[lane + 64] = v1;
+        if (lane >= 25 && lane < 37) {  // sin / cos of the joint angle this lane loaded
             double sn, cs;
-            sincos(a.qj[(size_t)rb * 12 + lane], &sn, &cs);
-            s.sc[lane][0] = sn;
-            s.sc[lane][1] = cs;
+            sincos(v0, &sn, &cs);
+            s.sc[lane - 25][0] = sn;
+            s.sc[lane - 25][1] = cs;
         }
         const bool anybad = wave_any(bad);
         if (lane == 0) { P.flags = anybad ? 1.0 : 0.0; P.kappa = (double)kap; }
@@ -477,11 +481,17 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
     UST(a, rb, 4);
     double Ic[9], Icinv[9];
     {
-        double t[6] = {0, 0, 0, 0, 0, 0};
-#pragma unroll 1
-        for (int b = 0; b < 13; ++b)
+        double t[6] = {0, 0, 0, 0, 0, 0}, t2[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int b = 0; b < 13; b += 2)
 #pragma unroll
             for (int k = 0; k < 6; ++k) t[k] += s.contrib[b][k];
+#pragma unroll
+        for (int b = 1; b < 13; b += 2)
+#pragma unroll
+            for (int k = 0; k < 6; ++k) t2[k] += s.contrib[b][k];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) t[k] += t2[k];
         Ic[0] = t[0]; Ic[4] = t[1]; Ic[8] = t[2];
         Ic[1] = Ic[3] = t[3]; Ic[2] = Ic[6] = t[4]; Ic[5] = Ic[7] = t[5];
         inv3(Ic, Icinv);
@@ -543,10 +553,19 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
     wsync();
     UST(a, rb, 6);
     double hb[6] = {0, 0, 0, 0, 0, 0};
-#pragma unroll 1
-    for (int b = 0; b < 13; ++b)
+    {
+        double h2[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
-        for (int k = 0; k < 6; ++k) hb[k] += s.contrib[b][k];
+        for (int b = 0; b < 13; b += 2)
+#pragma unroll
+            for (int k = 0; k < 6; ++k) hb[k] += s.contrib[b][k];
+#pragma unroll
+        for (int b = 1; b < 13; b += 2)
+#pragma unroll
+            for (int k = 0; k < 6; ++k) h2[k] += s.contrib[b][k];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) hb[k] += h2[k];
+    }
 
     // y = Tdot_inv(previous cycle) nu  (quirk A.3: nu, not T nu; one-cycle lag)
     double y[6] = {0, 0, 0, 0, 0, 0};
@@ -584,9 +603,14 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
         zeta[0] = hp[0] * inv_m; zeta[1] = hp[1] * inv_m; zeta[2] = hp[2] * inv_m;
         mv3(Icinv, hca, &zeta[3]);
     }
-    if (lane == 0) {
+    if (lane < 3) {  // eulAnglesRPY (cpp:12-20): roll, pitch, yaw on lanes 0, 1, 2 in parallel
         double RB[9];
         quat_R(s.in[3], s.in[4], s.in[5], s.in[6], RB);
+        const double ya = (lane == 0) ? RB[7] : ((lane == 1) ? -RB[6] : RB[3]);
+        const double xa = (lane == 0) ? RB[8] : ((lane == 1) ? sqrt(RB[7] * RB[7] + RB[8] * RB[8]) : RB[0]);
+        s.cen[CEN_POSE + 3 + lane] = atan2(ya, xa);
+    }
+    if (lane == 0) {
         double* cen = s.cen;
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
@@ -597,9 +621,6 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
             cen[CEN_VC + i] = cd[i];    // centerOfMassVelocity_ = [c_dot; omega_B] (cpp:261, quirk A.4)
             cen[CEN_VC + 3 + i] = wB[i];
         }
-        cen[CEN_POSE + 3] = atan2(RB[7], RB[8]);
-        cen[CEN_POSE + 4] = atan2(-RB[6], sqrt(RB[7] * RB[7] + RB[8] * RB[8]));
-        cen[CEN_POSE + 5] = atan2(RB[3], RB[0]);
 #pragma unroll
         for (int i = 0; i < 6; ++i) cen[CEN_HB + i] = hp[i];
         P.m = m; P.inv_m = inv_m;
@@ -1134,6 +1155,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
     // is computed here in one pass: Householder QR of the equality columns (column broadcast
     // through LDS), then R^-T v = -s_E, u = R^-1 v and s += C^T [v; 0] in closed form.
     // Redundant equalities (|d2| ~ 0) are skipped and must be consistent, as in the loop.
+    EST(a, rb, 0);
     if (!done && mp.neq > 0) {
         int myslot = -1;
         bool redundant = false;
@@ -1143,19 +1165,15 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
 #pragma unroll
         for (int e = 0; e < 12; ++e) {
             if (e < mp.neq && q == e) {
-                if (lane == e) {
-#pragma unroll
-                    for (int k = e & ~1; k < NQ; ++k) s.colbuf[k] = cc[k];
-                }
-                wsync();
-                double d[NQ];
+                // every lane forms the tail norm of its own column; lane e's is |d2|^2, so the
+                // reflector scalars start while the column itself is being broadcast (v_readlane)
                 double zp[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-                for (int k = 0; k < NQ; ++k) {
-                    d[k] = (k >= e) ? s.colbuf[k] : 0.0;
-                    zp[k & 3] += d[k] * d[k];
-                }
-                const double zn = (zp[0] + zp[1]) + (zp[2] + zp[3]);
+                for (int k = e; k < NQ; ++k) zp[k & 3] += cc[k] * cc[k];
+                const double zn = bcast((zp[0] + zp[1]) + (zp[2] + zp[3]), e);
+                double d[NQ];
+#pragma unroll
+                for (int k = 0; k < NQ; ++k) d[k] = (k >= e) ? bcast(cc[k], e) : 0.0;
                 const bool add = !(zn <= tiny * fmax(1.0, bcast(nn, e)));
                 // Householder reflection on rows e..23 (static q = e)
                 {
@@ -1180,9 +1198,9 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
                     redundant = true;
                 }
                 e0 = e + 1;
-                wsync();  // colbuf is rewritten next
             }
         }
+        EST(a, rb, 1);
         // general path (after a redundant equality): dynamic slot q
 #pragma unroll 1
         for (int e = e0; e < mp.neq; ++e) {
@@ -1214,6 +1232,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
             wsync();  // colbuf is rewritten next
         }
         neq_added = q;
+        EST(a, rb, 2);
         // R columns and equality slacks by slot
         if (myslot >= 0) {
 #pragma unroll
@@ -1238,6 +1257,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
             v[j] = in ? (-sj - ((av[0] + av[1]) + (av[2] + av[3]))) * ird : 0.0;
             y[j] = in ? (((lane == j) ? 1.0 : 0.0) - ((ay[0] + ay[1]) + (ay[2] + ay[3]))) * ird : 0.0;
         }
+        EST(a, rb, 3);
         double uu[4] = {0.0, 0.0, 0.0, 0.0}, ds[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int j = 0; j < 12; ++j) {
@@ -1254,6 +1274,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
         if (wave_any(bad)) { status = WBC_QP_INFEASIBLE; done = true; }
         wsync();
     }
+    EST(a, rb, 4);
     IST_DECL;
 
     while (!done) {

@@ -28,3 +28,7 @@ un = ["inputs+sincos", "stage A (leg chains)", "stage B (bodies)", "Jf + CoM sum
       "hb sum, y, zeta, lane0", "Jbar/Mbar/bbar", "Tdot_inv", "bounds, wrench, history"]
 du = np.diff(u, axis=1)
 print(json.dumps({n: float(np.median(du[:, i])) for i, n in enumerate(un)}, indent=1))
+q = e.debug()[:, 20:25]
+qn = ["eq fast path (Householder)", "eq generic path", "R/s to LDS + substitutions", "u, R^-1 rows, slacks"]
+dq = np.diff(q, axis=1)
+print(json.dumps({n: float(np.median(dq[:, i])) for i, n in enumerate(qn)}, indent=1))
