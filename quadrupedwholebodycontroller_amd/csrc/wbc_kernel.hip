@@ -42,8 +42,10 @@ struct Body {  // body quantities after stage B
     double c[3], I[9], F[3], N[3], pad[6];
 };
 static_assert(sizeof(Frame) == sizeof(Body), "frame / body union");
+static_assert(sizeof(wbc_model) % 16 == 0, "model staged as double2");
 
 struct UpdScratch {
+    wbc_model mdl;          // model constants, staged from global memory (per-lane indexed reads)
     double in[92];          // pose 7 | nu 18 | q 12 | ref 54
     double sc[12][2];       // sin, cos of q_j
     union {
@@ -59,7 +61,6 @@ struct UpdScratch {
     double KA[12][3];       // I_c^-1 A_ang
     double Mjj[12][3];      // leg block rows of M
     double hj[12];          // joint bias (C nu)_j
-    double contrib[13][6];  // per-body partial sums
     double cen[40];         // uniform scratch (CEN_*)
 };
 
@@ -137,6 +138,16 @@ __device__ __forceinline__ void wave_argmin(double& v, int& i) {
     i = bi;
 }
 __device__ __forceinline__ bool wave_any(bool p) { return __any(p); }
+
+// Sum over the 16 lanes of each DPP row (row_ror 8, 4, 2, 1); lane 0's value is broadcast so the
+// result is uniform.  Used for the 13-body sums of the update phase (lanes >= 13 pass 0).
+__device__ __forceinline__ double row0_sum(double v) {
+    v += dpp_d<0x128>(v);
+    v += dpp_d<0x124>(v);
+    v += dpp_d<0x122>(v);
+    v += dpp_d<0x121>(v);
+    return bcast(v, 0);
+}
 
 // XCD-aware robot index (optional, -DWBC_XCD_REMAP=1).  Workgroups are dealt round-robin to the
 // 8 XCDs (blockIdx % 8), each with its own L2; the remap gives every XCD a contiguous range of
@@ -290,7 +301,7 @@ __device__ __forceinline__ double sel3(const double* v, int k) { return k == 0 ?
 __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
     UpdScratch& s = L.u;
     Prob& P = L.prob;
-    const wbc_model& md = *a.model;
+    const wbc_model& md = s.mdl;  // LDS copy, filled below
     const wbc_params& pr = *a.params;
     const int lane = lane_id();
     const int kap = a.contacts[rb];
@@ -311,6 +322,15 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
         const bool two = lane + 64 < 91;
         const double v0 = *p0;
         const double v1 = two ? a.ref[(size_t)rb * 54 + (lane + 64 - 37)] : 0.0;
+        {   // the model (shared by all robots, L2-resident) into LDS: the update phase indexes it
+            // per lane (leg / body), which from global memory would be a vector load each time
+            constexpr int N2 = (int)(sizeof(wbc_model) / sizeof(double2));
+            const double2* src = reinterpret_cast<const double2*>(a.model);
+            double2* dst = reinterpret_cast<double2*>(&s.mdl);
+#pragma unroll
+            for (int k = 0; k < N2; k += 64)
+                if (k + lane < N2) dst[k + lane] = src[k + lane];
+        }
         const bool bad = !isfinite(v0) || !isfinite(v1);
         s.in[lane] = v0;
         if (two) s.in[lane + 64] = v1;
@@ -331,9 +351,21 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
     const double* qd = &s.in[13];
     const double* ref = &s.in[37];
 
-    // stage A: one lane per leg walks HAA -> HFE -> KFE; lane 4 writes the base frame
+    // stage A: one lane per leg walks HAA -> HFE -> KFE; lane 4 writes the base frame.
+    // The joint-local factors (link rotation x joint rotation, axis in the parent frame) do not
+    // depend on the chain and are formed first, so each link adds one 3x3 product to the
+    // dependent chain instead of two.
     if (lane < 4) {
         const int l = lane;
+        double Lk[3][9], axl[3][3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const wbc_link& lk = md.link[l][k];
+            double Rl[9];
+            axis_rot(lk.axis, s.sc[3 * l + k][0], s.sc[3 * l + k][1], Rl);
+            mm3(lk.R, Rl, Lk[k]);
+            mv3(lk.R, lk.axis, axl[k]);
+        }
         double Rp[9], op[3], wp[3], alp[3] = {0, 0, 0}, aop[3] = {0, 0, 0}, vop[3];
         quat_R(s.in[3], s.in[4], s.in[5], s.in[6], Rp);
 #pragma unroll
@@ -342,15 +374,11 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
         for (int k = 0; k < 3; ++k) {
             const wbc_link& lk = md.link[l][k];
             const int j = 3 * l + k;
-            double Rj[9], Rl[9], oj[3], aj[3], rel[3], t[3], u[3];
-            mm3(Rp, lk.R, Rj);
-            mv3(Rp, lk.p, oj);
-            oj[0] += op[0]; oj[1] += op[1]; oj[2] += op[2];
-            mv3(Rj, lk.axis, aj);
-            axis_rot(lk.axis, s.sc[j][0], s.sc[j][1], Rl);
-            mm3(Rj, Rl, Rp);  // child body orientation
+            double rel[3], aj[3], t[3], u[3], Rn[9];
+            mv3(Rp, lk.p, rel);       // joint origin - parent origin (world)
+            mv3(Rp, axl[k], aj);      // joint axis (world)
+            mm3(Rp, Lk[k], Rn);       // child body orientation
             const double qdk = qd[j];
-            rel[0] = oj[0] - op[0]; rel[1] = oj[1] - op[1]; rel[2] = oj[2] - op[2];
             // the joint origin is a point of the parent: velocity / acceleration at nu_dot = 0
             cross3(wp, rel, t);
             cross3(wp, t, u);
@@ -363,9 +391,11 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
             for (int i = 0; i < 3; ++i) {
                 alp[i] += t[i] * qdk;
                 wp[i] += aj[i] * qdk;
-                op[i] = oj[i];
+                op[i] += rel[i];
                 aop[i] = ao[i];
             }
+#pragma unroll
+            for (int i = 0; i < 9; ++i) Rp[i] = Rn[i];
             Frame& f = s.fr[1 + j];
 #pragma unroll
             for (int i = 0; i < 9; ++i) f.R[i] = Rp[i];
@@ -385,8 +415,9 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
 
     UST(a, rb, 2);
     // stage B: one lane per body: com, world inertia, com velocity, m a_com, I alpha + w x I w
+    double c[3] = {0, 0, 0}, cd[3] = {0, 0, 0};  // CoM and its velocity (cpp:260-261)
     {
-        double c[3], I[9], vc[3], F[3], N[3], mb = 0.0;
+        double cb[3] = {0, 0, 0}, I[9], vc[3] = {0, 0, 0}, F[3], N[3], mb = 0.0;
         if (lane < 13) {
             const Frame& f = s.fr[lane];
             const double* com;
@@ -403,7 +434,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
             for (int i = 0; i < 3; ++i) { o[i] = f.o[i]; w[i] = f.w[i]; al[i] = f.al[i]; ao[i] = f.ao[i]; vo[i] = f.vo[i]; }
             mv3(R, com, rel);
 #pragma unroll
-            for (int i = 0; i < 3; ++i) c[i] = o[i] + rel[i];
+            for (int i = 0; i < 3; ++i) cb[i] = o[i] + rel[i];
             rot_inertia(R, Il, I);
             cross3(w, rel, t);
             cross3(w, t, u);
@@ -432,11 +463,15 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
         if (lane < 13) {
             Body& bd = s.bd[lane];
 #pragma unroll
-            for (int i = 0; i < 3; ++i) { bd.c[i] = c[i]; bd.F[i] = F[i]; bd.N[i] = N[i]; }
+            for (int i = 0; i < 3; ++i) { bd.c[i] = cb[i]; bd.F[i] = F[i]; bd.N[i] = N[i]; }
 #pragma unroll
             for (int i = 0; i < 9; ++i) bd.I[i] = I[i];
+        }
+        // mass-weighted sums over the 13 bodies (lanes >= 13 hold mb = 0)
 #pragma unroll
-            for (int i = 0; i < 3; ++i) { s.contrib[lane][i] = mb * c[i]; s.contrib[lane][3 + i] = mb * vc[i]; }
+        for (int i = 0; i < 3; ++i) {
+            cd[i] = row0_sum(mb * vc[i]);
+            c[i] = row0_sum(mb * cb[i]);
         }
     }
     wsync();
@@ -449,60 +484,48 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
 #pragma unroll
         for (int r = 0; r < 3; ++r) s.Jf[l][3 * r + k] = col[r];
     }
-    // CoM and its velocity (getCenterOfMassPosition/Velocity, cpp:260-261)
-    double c[3] = {0, 0, 0}, cd[3] = {0, 0, 0};
     double m = md.base_mass;
 #pragma unroll
     for (int l = 0; l < 4; ++l)
 #pragma unroll
         for (int k = 0; k < 3; ++k) m += md.link[l][k].mass;
-#pragma unroll 1
-    for (int b = 0; b < 13; ++b)
-#pragma unroll
-        for (int i = 0; i < 3; ++i) { c[i] += s.contrib[b][i]; cd[i] += s.contrib[b][3 + i]; }
     const double inv_m = 1.0 / m;
 #pragma unroll
     for (int i = 0; i < 3; ++i) { c[i] *= inv_m; cd[i] *= inv_m; }
     const double r[3] = {c[0] - pB[0], c[1] - pB[1], c[2] - pB[2]};
-    wsync();  // contrib is reused
-    if (lane < 13) {  // centroidal inertia contributions
-        const double mb = (lane == 0) ? md.base_mass : md.link[(lane - 1) / 3][(lane - 1) % 3].mass;
-        const Body& bd = s.bd[lane];
-        double d[3] = {bd.c[0] - c[0], bd.c[1] - c[1], bd.c[2] - c[2]};
-        const double dd = dot3(d, d);
-        s.contrib[lane][0] = bd.I[0] + mb * (dd - d[0] * d[0]);
-        s.contrib[lane][1] = bd.I[4] + mb * (dd - d[1] * d[1]);
-        s.contrib[lane][2] = bd.I[8] + mb * (dd - d[2] * d[2]);
-        s.contrib[lane][3] = bd.I[1] - mb * d[0] * d[1];
-        s.contrib[lane][4] = bd.I[2] - mb * d[0] * d[2];
-        s.contrib[lane][5] = bd.I[5] - mb * d[1] * d[2];
-    }
-    wsync();
     UST(a, rb, 4);
     double Ic[9], Icinv[9];
-    {
-        double t[6] = {0, 0, 0, 0, 0, 0}, t2[6] = {0, 0, 0, 0, 0, 0};
+    {   // centroidal inertia: parallel-axis contributions of the 13 bodies, summed across lanes
+        double t[6] = {0, 0, 0, 0, 0, 0};
+        if (lane < 13) {
+            const double mb = (lane == 0) ? md.base_mass : md.link[(lane - 1) / 3][(lane - 1) % 3].mass;
+            const Body& bd = s.bd[lane];
+            double d[3] = {bd.c[0] - c[0], bd.c[1] - c[1], bd.c[2] - c[2]};
+            const double dd = dot3(d, d);
+            t[0] = bd.I[0] + mb * (dd - d[0] * d[0]);
+            t[1] = bd.I[4] + mb * (dd - d[1] * d[1]);
+            t[2] = bd.I[8] + mb * (dd - d[2] * d[2]);
+            t[3] = bd.I[1] - mb * d[0] * d[1];
+            t[4] = bd.I[2] - mb * d[0] * d[2];
+            t[5] = bd.I[5] - mb * d[1] * d[2];
+        }
 #pragma unroll
-        for (int b = 0; b < 13; b += 2)
-#pragma unroll
-            for (int k = 0; k < 6; ++k) t[k] += s.contrib[b][k];
-#pragma unroll
-        for (int b = 1; b < 13; b += 2)
-#pragma unroll
-            for (int k = 0; k < 6; ++k) t2[k] += s.contrib[b][k];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) t[k] += t2[k];
+        for (int k = 0; k < 6; ++k) t[k] = row0_sum(t[k]);
         Ic[0] = t[0]; Ic[4] = t[1]; Ic[8] = t[2];
         Ic[1] = Ic[3] = t[3]; Ic[2] = Ic[6] = t[4]; Ic[5] = Ic[7] = t[5];
         inv3(Ic, Icinv);
     }
-    wsync();
-    if (lane < 13) {  // base bias: sum F ; sum (c_b - p_B) x F + N
-        const Body& bd = s.bd[lane];
-        double rb_[3] = {bd.c[0] - pB[0], bd.c[1] - pB[1], bd.c[2] - pB[2]}, t[3];
-        cross3(rb_, bd.F, t);
+    double hb[6] = {0, 0, 0, 0, 0, 0};  // base bias: sum F ; sum (c_b - p_B) x F + N
+    {
+        if (lane < 13) {
+            const Body& bd = s.bd[lane];
+            double rb_[3] = {bd.c[0] - pB[0], bd.c[1] - pB[1], bd.c[2] - pB[2]}, t[3];
+            cross3(rb_, bd.F, t);
 #pragma unroll
-        for (int i = 0; i < 3; ++i) { s.contrib[lane][i] = bd.F[i]; s.contrib[lane][3 + i] = t[i] + bd.N[i]; }
+            for (int i = 0; i < 3; ++i) { hb[i] = bd.F[i]; hb[3 + i] = t[i] + bd.N[i]; }
+        }
+#pragma unroll
+        for (int k = 0; k < 6; ++k) hb[k] = row0_sum(hb[k]);
     }
     UST(a, rb, 5);
     // stage C: per joint: centroidal momentum column (about c), leg block of M, joint bias (C nu)_j
@@ -552,20 +575,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
     }
     wsync();
     UST(a, rb, 6);
-    double hb[6] = {0, 0, 0, 0, 0, 0};
-    {
-        double h2[6] = {0, 0, 0, 0, 0, 0};
-#pragma unroll
-        for (int b = 0; b < 13; b += 2)
-#pragma unroll
-            for (int k = 0; k < 6; ++k) hb[k] += s.contrib[b][k];
-#pragma unroll
-        for (int b = 1; b < 13; b += 2)
-#pragma unroll
-            for (int k = 0; k < 6; ++k) h2[k] += s.contrib[b][k];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) hb[k] += h2[k];
-    }
+
 
     // y = Tdot_inv(previous cycle) nu  (quirk A.3: nu, not T nu; one-cycle lag)
     double y[6] = {0, 0, 0, 0, 0, 0};
@@ -1466,7 +1476,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
                     for (int i = 0; i < 3; ++i) { F[i] += fl[i]; Mm[i] += t[i]; }
                 }
             }
-            if (lane < 3) xv = sel3(F, lane) * inv_m - (lane == 2 ? pr.gravity : 0.0);
+            if (lane < 3) xv = sel3(F, lane) * P.inv_m - (lane == 2 ? pr.gravity : 0.0);
             else {
                 const int rr = lane - 3;
                 xv = P.Icinv[3 * rr] * Mm[0] + P.Icinv[3 * rr + 1] * Mm[1] + P.Icinv[3 * rr + 2] * Mm[2];
