@@ -139,6 +139,33 @@ __device__ __forceinline__ void wave_argmin(double& v, int& i) {
 }
 __device__ __forceinline__ bool wave_any(bool p) { return __any(p); }
 
+// Wave argmin as a plain fp64 min: the lane index is written into the 6 low mantissa bits (as
+// 63 - lane for negative values, so ties go to the lowest lane either way), then v_min_f64 over
+// row_ror 8/4/2/1 and row_bcast 15/31 leaves the minimum in lane 63.  18 VALU + 2 readlanes
+// instead of the compare/select ladder.  Returns the lane (uniform); callers re-read the exact
+// value from that lane when they need it.  v must not be NaN.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_min(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(__double2loint(v), __double2loint(v), CTRL, ROWMASK, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(v), __double2hiint(v), CTRL, ROWMASK, 0xF, false);
+    return fmin(v, __hiloint2double(hi, lo));
+}
+__device__ __forceinline__ int wave_argmin_lane(double v) {
+    const int lane = lane_id();
+    const int hi = __double2hiint(v);
+    const int tag = (hi < 0) ? (63 - lane) : lane;
+    v = __hiloint2double(hi, (__double2loint(v) & ~63) | tag);
+    v = dpp_min<0x128, 0xF>(v);  // row_ror:8
+    v = dpp_min<0x124, 0xF>(v);  // row_ror:4
+    v = dpp_min<0x122, 0xF>(v);  // row_ror:2
+    v = dpp_min<0x121, 0xF>(v);  // row_ror:1
+    v = dpp_min<0x142, 0xA>(v);  // row_bcast:15 into rows 1, 3
+    v = dpp_min<0x143, 0xC>(v);  // row_bcast:31 into rows 2, 3
+    const int mlo = __builtin_amdgcn_readlane(__double2loint(v), 63);
+    const int mhi = __builtin_amdgcn_readlane(__double2hiint(v), 63);
+    return (mhi < 0) ? (63 - (mlo & 63)) : (mlo & 63);
+}
+
 // Sum over the 16 lanes of each DPP row (row_ror 8, 4, 2, 1); lane 0's value is broadcast so the
 // result is uniform.  Used for the 13-body sums of the update phase (lanes >= 13 pass 0).
 __device__ __forceinline__ double row0_sum(double v) {
@@ -1304,9 +1331,8 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
                     const double tol = 1e-10 * fmax(1.0, fabs(bp));
                     if (sp < -tol) v = sp * inrm;
                 }
-                int idx = lane;
-                wave_argmin(v, idx);
-                if (!(v < 1e299)) break;  // no violated constraint: optimal
+                const int idx = wave_argmin_lane(v);
+                if (!(bcast(v, idx) < 1e299)) break;  // no violated constraint: optimal
                 pstar = idx;
                 up = 0.0;
             }
@@ -1338,12 +1364,12 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
             const double sps = bcast(sp, pstar);
             // partial step: keep active inequality multipliers >= 0
             double t1;
-            int l1 = lane;
+            int l1;
             {
                 double v = 1e300;
                 if (lane < q && lane >= neq_added && rk > 1e-14) v = u * fast_rcp(rk);
-                wave_argmin(v, l1);
-                t1 = v;
+                l1 = wave_argmin_lane(v);
+                t1 = bcast(v, l1);
             }
             {
                 const double t2 = (zn > tiny) ? (-sps * fast_rcp(zn)) : 1e300;
