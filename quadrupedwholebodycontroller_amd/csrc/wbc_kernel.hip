@@ -94,6 +94,11 @@ enum CenOff { CEN_C = 0, CEN_CD = 3, CEN_R = 6, CEN_HB = 9, CEN_POSE = 27, CEN_V
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ int lane_id() { return threadIdx.x; }
 __device__ __forceinline__ void wsync() { __syncthreads(); }  // one wave per workgroup
+// Ordering point for lane-to-lane exchange through LDS inside the (single-wave) workgroup: LDS
+// instructions of one wave execute in issue order, so only the compiler must not move LDS
+// accesses across this point; a wavefront-scope fence is exactly that (no s_waitcnt, unlike
+// __syncthreads, which also drains every outstanding global store).
+__device__ __forceinline__ void lds_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 
 __device__ __forceinline__ double bcast(double v, int lane) {
     int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
@@ -1138,7 +1143,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
             if (lane == k) zk = zz;
             if (lane > k) gsv -= hrow[k] * zz;
         }
-        wsync();  // L visible
+        lds_sync();  // L visible
         // back substitution L^T x = z: lane j holds column j of L below the diagonal (L[k][j], k > j)
         double lcol[12];
 #pragma unroll
@@ -1151,7 +1156,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
             if (lane < k) zt -= lcol[k] * xk;
         }
     }
-    wsync();
+    lds_sync();
 
     STAMP(a, rb, 2);
     double cc[NQ];
@@ -1173,7 +1178,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
     }
 
     zero_rinv(s);
-    wsync();
+    lds_sync();
     STAMP(a, rb, 3);
     // Goldfarb-Idnani (wave-uniform control flow).  After a drop the loop re-adds the remaining
     // active set (rebuild mode) through the same add path, then resumes the pending constraint.
@@ -1245,7 +1250,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
 #pragma unroll
                 for (int k = 0; k < NQ; ++k) s.colbuf[k] = cc[k];
             }
-            wsync();
+            lds_sync();
             double d[NQ];
 #pragma unroll
             for (int k = 0; k < NQ; ++k) d[k] = s.colbuf[k];
@@ -1266,7 +1271,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
             } else if (lane == e) {
                 redundant = true;
             }
-            wsync();  // colbuf is rewritten next
+            lds_sync();  // colbuf is rewritten next
         }
         neq_added = q;
         EST(a, rb, 2);
@@ -1276,7 +1281,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
             for (int k = 0; k < 12; ++k) s.Rm[myslot][k] = cc[k];
             s.colbuf[myslot] = sp;
         }
-        wsync();
+        lds_sync();
         // forward substitutions with R^T: v = -R^-T s_E (uniform) and, in lane i, row i of R^-1
         double v[12], y[12];
 #pragma unroll
@@ -1309,7 +1314,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
         sp += (ds[0] + ds[1]) + (ds[2] + ds[3]);
         const bool bad = redundant && !(fabs(sp) <= 1e-9 * fmax(1.0, fabs(bp)));
         if (wave_any(bad)) { status = WBC_QP_INFEASIBLE; done = true; }
-        wsync();
+        lds_sync();
     }
     EST(a, rb, 4);
     IST_DECL;
@@ -1407,7 +1412,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
                 ++q;
                 pstar = -1;
             }
-            wsync();
+            lds_sync();
         }
         if (drop) {
             // C restarts from C0 and the remaining active set is re-added (rebuild mode).
@@ -1420,7 +1425,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
             build_normal(P, mp, pr, pl, cc, bb, eqd);
             to_column(s, cc);  // fresh C0; slacks sp are kept
             zero_rinv(s);
-            wsync();
+            lds_sync();
             rbk = 0;
         }
         IST(5);  // bookkeeping, barrier, drop path
@@ -1430,9 +1435,9 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
     STAMP(a, rb, 4);
     // primal recovery: y = x0 + H^-1 w,  w = sum_k u_k n_{a_k}  (LDS transpose-sum over active rows)
     if (lane < 64) s.ucon[lane] = -1.0;  // slot index of constraint `lane` (or -1)
-    wsync();
+    lds_sync();
     if (lane < q && act >= 0) s.ucon[act] = (double)lane;
-    wsync();
+    lds_sync();
     {
         const int slot = is_con ? (int)s.ucon[lane] : -1;
         const double uk = __shfl(u, slot < 0 ? 0 : slot);  // multiplier held by the slot lane
@@ -1444,7 +1449,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
             for (int k = 0; k < NQ; ++k) s.Wt[slot][k] = uk * n[k];
         }
     }
-    wsync();
+    lds_sync();
     double wi = 0.0;  // w_i for lane i < 24
     if (lane < NQ) {
         double wp[4] = {0.0, 0.0, 0.0, 0.0};
@@ -1479,10 +1484,10 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
         }
         yv = (lane < 12) ? s.xs[lane < 12 ? lane : 0] + xk_own : 0.0;
     }
-    wsync();  // Wt (aliases Rinv) and ucon fully consumed
+    lds_sync();  // Wt (aliases Rinv) and ucon fully consumed
     double* yq = s.ucon;  // y[0..23]: qdd (w[0:12]) then slots
     if (lane < 12) { yq[lane] = wi; yq[12 + lane] = yv; }
-    wsync();
+    lds_sync();
 
     STAMP(a, rb, 5);
     // outputs: x (42, cpp:534-541), grf = x[18:30] (cpp:556-563), tau (cpp:565-576)
