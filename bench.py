@@ -59,9 +59,9 @@ def cpu_baseline(inp, budget_s=15.0):
             wbc_ref.run_batch(sub)
             dt = time.perf_counter() - t0
             t_used += dt
-            if dt >= budget_s / 4 or t_used >= budget_s:
+            if dt >= 0.8 * budget_s or t_used >= 2.5 * budget_s:
                 break
-            n = int(n * max(2.0, min(10.0, (budget_s / 4) / max(dt, 1e-6))))
+            n = int(n * max(2.0, min(10.0, budget_s / max(dt, 1e-6))))
         return dict(value=n / dt, unit="solves/s", cores=1, kind="port",
                     sample=f"{n} cold solves of the same workload through oracle/wbc_ref.c "
                            f"(dense reference-faithful restatement, -O3), 1 thread, {dt:.2f} s")
@@ -82,8 +82,8 @@ def cpu_baseline(inp, budget_s=15.0):
 
 
 def committed_traffic(workload, batch):
-    """HBM bytes per launch of wbc_step_kernel from a committed PMC summary (tools/pmc_summary.py)
-    taken on this exact kernel source, workload and batch; None if there is none."""
+    """HBM bytes per launch, per kernel and per step, from a committed PMC summary
+    (tools/pmc_summary.py) taken on this exact kernel source, workload and batch; {} if none."""
     import glob
 
     sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -96,9 +96,9 @@ def committed_traffic(workload, batch):
         except (OSError, ValueError):
             continue
         if (rec.get("kernel_source_sha256") == want and rec.get("workload") == workload and
-                rec.get("batch") == batch and "traffic_bytes_per_launch" in rec):
-            return rec["traffic_bytes_per_launch"], os.path.relpath(f, ROOT)
-    return None, None
+                rec.get("batch") == batch and "traffic" in rec):
+            return rec["traffic"], os.path.relpath(f, ROOT)
+    return {}, None
 
 
 def bench_trot(torch, stream, device, STATELESS, B=4096, T=400, seed=2):
@@ -166,7 +166,7 @@ def main():
     else:
         torch.cuda.set_device(local_rank)
 
-    from quadrupedwholebodycontroller_amd import NO_X, STATELESS, Engine, workloads
+    from quadrupedwholebodycontroller_amd import NO_X, SPLIT, STATELESS, Engine, workloads
 
     STEP_FLAGS = STATELESS | NO_X  # cold solves; outputs tau, grf, status, iters (the published ones)
 
@@ -211,39 +211,33 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
-    # kernel duration for the roofline: HIP events on the launch stream around K back-to-back
-    # launches of the step kernel (the engine's only kernel per step).  This includes the few-us
-    # dispatch gap between launches; rocprofv3's per-dispatch average (profiles/) excludes it.
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record(stream)
-    for _ in range(args.steps):
-        e.step(STEP_FLAGS)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    # Kernel duration for the roofline: HIP events on the launch stream around K back-to-back
+    # launches of the step kernel (the engine's only kernel per step; this includes the few-us
+    # dispatch gap between launches, which rocprofv3's per-dispatch average in profiles/ excludes).
+    def timed(fn):
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        for _ in range(args.steps):
+            fn()
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        return ev0.elapsed_time(ev1) / args.steps
+
+    step_ms = timed(lambda: e.step(STEP_FLAGS))
     out = e.outputs()
     iters = out["iters"].astype(np.int64)
     status = out["status"]
-    flops = float(np.sum(F_DYN + F_ASM + F_TAU + F_FACT + F_ITER * iters))
-    achieved_tf = flops / (kernel_ms * 1e-3) / 1e12
-    hbm_gbs = B * BYTES_COLD / (kernel_ms * 1e-3) / 1e9
+    flops_step = float(np.sum(F_DYN + F_ASM + F_TAU + F_FACT + F_ITER * iters))
+    tf_step = flops_step / (step_ms * 1e-3) / 1e12
+    hbm_gbs = B * BYTES_COLD / (step_ms * 1e-3) / 1e9
 
     breakdown = None
-    if args.breakdown:
-        ev0.record(stream)
-        for _ in range(args.steps):
-            e.update(STATELESS)
-        ev1.record(stream)
-        torch.cuda.synchronize()
-        upd_ms = ev0.elapsed_time(ev1) / args.steps
-        ev0.record(stream)
-        for _ in range(args.steps):
-            e.update(STATELESS)
-            e.solve(STATELESS)
-        ev1.record(stream)
-        torch.cuda.synchronize()
-        both_ms = ev0.elapsed_time(ev1) / args.steps
-        breakdown = dict(update_kernel_ms=upd_ms, solve_kernel_ms=both_ms - upd_ms, fused_kernel_ms=kernel_ms)
+    if args.breakdown:  # the same step as two kernels: update (dynamics + assembly) and solve (QP + torques)
+        upd_ms = timed(lambda: e.update(STEP_FLAGS))
+        solve_ms = timed(lambda: e.solve(STEP_FLAGS))  # re-solves the assembled problem (stateless)
+        split_ms = timed(lambda: e.step(STEP_FLAGS | SPLIT))
+        breakdown = dict(update_kernel_ms=upd_ms, solve_kernel_ms=solve_ms, split_step_ms=split_ms,
+                         fused_step_ms=step_ms)
 
     extra = {}
     if args.extra and rank == 0:
@@ -259,12 +253,7 @@ def main():
             e2.set_reference(inp2["ref"], inp2["contacts"], inp2["switching"])
             for _ in range(args.warmup):
                 e2.step(STEP_FLAGS)
-            ev0.record(stream)
-            for _ in range(args.steps):
-                e2.step(STEP_FLAGS)
-            ev1.record(stream)
-            torch.cuda.synchronize()
-            ms2 = ev0.elapsed_time(ev1) / args.steps
+            ms2 = timed(lambda: e2.step(STEP_FLAGS))
             o2 = e2.outputs()
             extra[name] = dict(batch=B2, ms_per_step=ms2, solves_per_s=B2 / (ms2 * 1e-3),
                                status_counts=np.bincount(o2["status"], minlength=4).tolist(),
@@ -290,13 +279,15 @@ def main():
         "config": {"workload": args.config, "description": cfg["desc"], "batch_per_gpu": B,
                    "global_batch": B * world, "parallelism": f"dp{world} (robot shards) + RCCL all-gather of tau"
                    if world > 1 else "dp1"},
-        "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": "wbc_step_kernel", "kernel_ms": kernel_ms,
+        "roofline": {"bound": "mfma", "achieved": tf_step, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": tf_step / FP64_PEAK_TFLOPS, "traffic": traffic.get("wbc_step_kernel"),
+                     "traffic_source": traffic_src, "kernel": "wbc_step_kernel", "kernel_ms": step_ms,
                      "note": "fp64 compute roof (gfx950 fp64 vector = matrix peak); algorithmic flops F(k) of "
-                             "SURVEY 8(d), k = iters[] per robot; the path is latency-bound, not HBM-bound"},
+                             "SURVEY 8(d), k = iters[] per robot; latency/issue-bound small dense linear algebra"},
         "roofline_hbm": {"bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": hbm_gbs / HBM_PEAK_GBS, "bytes_per_solve": BYTES_COLD, "traffic": traffic},
+                         "frac": hbm_gbs / HBM_PEAK_GBS, "bytes_per_solve": BYTES_COLD,
+                         "traffic": traffic.get("wbc_step_kernel"),
+                         "note": "algorithmic 929 B/solve over the kernel time; traffic = PMC bytes per launch"},
         "qp_status_counts": np.bincount(status, minlength=4).tolist(),
         "mean_iters": float(iters.mean()),
     }

@@ -106,6 +106,8 @@ enum {
 #define WBC_STATELESS 1u /* cold step: history = reset values; history is neither read nor written */
 #define WBC_DEBUG 2u     /* also write the per-robot debug record (wbc_get_debug) */
 #define WBC_NO_X 4u      /* skip the x[42] output (tau, grf, status, iters are still written) */
+#define WBC_SPLIT 8u     /* wbc_step as the update kernel + solve kernel pair instead of one fused kernel */
+#define WBC_TIMED 16u    /* wbc_step records HIP events around its kernels (wbc_last_kernel_ms) */
 
 /* Debug record layout (doubles per robot), written by update/step under WBC_DEBUG. */
 enum {
@@ -164,7 +166,8 @@ int32_t wbc_reset(wbc_engine* h, const uint8_t* mask);
 int32_t wbc_update(wbc_engine* h, uint32_t flags);
 /* solveQP() + computeJointTorques() on the problem assembled by the last wbc_update. */
 int32_t wbc_solve(wbc_engine* h, uint32_t flags);
-/* Fused update + solve + torques: the fast path. */
+/* update + solve + torques for one control cycle: one fused kernel (the problem stays in LDS), or
+ * under WBC_SPLIT the update kernel then the solve kernel (the problem passes through HBM). */
 int32_t wbc_step(wbc_engine* h, uint32_t flags);
 int32_t wbc_synchronize(wbc_engine* h);
 
@@ -178,7 +181,7 @@ int32_t wbc_device_outputs(wbc_engine* h, double** d_tau, double** d_grf, double
 /* Debug records [B][WBC_DBG_LEN] of the last update/step run with WBC_DEBUG. */
 int32_t wbc_get_debug(wbc_engine* h, double* out);
 
-/* Launch statistics of the last wbc_step (ms, HIP events on the engine stream). */
+/* Device time of the last wbc_step run with WBC_TIMED (ms, HIP events on the engine stream). */
 int32_t wbc_last_kernel_ms(wbc_engine* h, double* ms);
 const char* wbc_last_error(void);
 

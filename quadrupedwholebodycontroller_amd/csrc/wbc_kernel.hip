@@ -42,10 +42,8 @@ struct Body {  // body quantities after stage B
     double c[3], I[9], F[3], N[3], pad[6];
 };
 static_assert(sizeof(Frame) == sizeof(Body), "frame / body union");
-static_assert(sizeof(wbc_model) % 16 == 0, "model staged as double2");
 
 struct UpdScratch {
-    wbc_model mdl;          // model constants, staged from global memory (per-lane indexed reads)
     double in[92];          // pose 7 | nu 18 | q 12 | ref 54
     double sc[12][2];       // sin, cos of q_j
     union {
@@ -330,10 +328,8 @@ __device__ __forceinline__ double sel3(const double* v, int k) { return k == 0 ?
 // update phase (≙ updateState, cpp:256-294, plus the per-cycle terms of solveQP that do not
 // depend on the QP: computeDesiredWrench cpp:426-445, swing commands cpp:447-464, bounds cpp:503-515)
 // ---------------------------------------------------------------------------------------
-__device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
-    UpdScratch& s = L.u;
-    Prob& P = L.prob;
-    const wbc_model& md = s.mdl;  // LDS copy, filled below
+__device__ void update_phase(const KernelArgs& a, int rb, UpdScratch& s, Prob& P) {
+    const wbc_model& md = *a.model;
     const wbc_params& pr = *a.params;
     const int lane = lane_id();
     const int kap = a.contacts[rb];
@@ -354,15 +350,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, Lds& L) {
         const bool two = lane + 64 < 91;
         const double v0 = *p0;
         const double v1 = two ? a.ref[(size_t)rb * 54 + (lane + 64 - 37)] : 0.0;
-        {   // the model (shared by all robots, L2-resident) into LDS: the update phase indexes it
-            // per lane (leg / body), which from global memory would be a vector load each time
-            constexpr int N2 = (int)(sizeof(wbc_model) / sizeof(double2));
-            const double2* src = reinterpret_cast<const double2*>(a.model);
-            double2* dst = reinterpret_cast<double2*>(&s.mdl);
-#pragma unroll
-            for (int k = 0; k < N2; k += 64)
-                if (k + lane < N2) dst[k + lane] = src[k + lane];
-        }
+
         const bool bad = !isfinite(v0) || !isfinite(v1);
         s.in[lane] = v0;
         if (two) s.in[lane + 64] = v1;
@@ -1065,9 +1053,7 @@ __device__ __forceinline__ void add_column(QpScratch& s, int q, bool add, double
     }
 }
 
-__device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
-    const Prob& P = L.prob;
-    QpScratch& s = L.q;
+__device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratch& s) {
     const wbc_params& pr = *a.params;
     const int lane = lane_id();
     const int kap = (int)P.kappa;
@@ -1545,37 +1531,53 @@ __device__ void solve_phase(const KernelArgs& a, int rb, Lds& L) {
 // ---------------------------------------------------------------------------------------
 #define WBC_KERNEL_ATTR \
     __global__ __attribute__((amdgpu_flat_work_group_size(64, 64), amdgpu_waves_per_eu(WBC_WAVES_PER_SIMD)))
+// Update-kernel occupancy: 2, 3 and 4 waves per SIMD time the same (the phase is VALU-bound,
+// profiles/r01/split_probe.log); 2 keeps it spill-free
+#ifndef WBC_UPDATE_WAVES_PER_SIMD
+#define WBC_UPDATE_WAVES_PER_SIMD 2
+#endif
+#define WBC_UPDATE_KERNEL_ATTR \
+    __global__ __attribute__((amdgpu_flat_work_group_size(64, 64), amdgpu_waves_per_eu(WBC_UPDATE_WAVES_PER_SIMD)))
+
+struct UpdLds {
+    Prob prob;
+    UpdScratch u;
+};
+struct SolveLds {
+    Prob prob;
+    QpScratch q;
+};
 
 WBC_KERNEL_ATTR void wbc_step_kernel(KernelArgs a) {
     __shared__ Lds L;
     const int rb = xcd_robot();
     if (rb >= a.batch) return;
     STAMP(a, rb, 0);
-    update_phase(a, rb, L);
+    update_phase(a, rb, L.u, L.prob);
     STAMP(a, rb, 1);
-    solve_phase(a, rb, L);
+    solve_phase(a, rb, L.prob, L.q);
     STAMP(a, rb, 6);
 }
 
-WBC_KERNEL_ATTR void wbc_update_kernel(KernelArgs a) {
-    __shared__ Lds L;
+WBC_UPDATE_KERNEL_ATTR void wbc_update_kernel(KernelArgs a) {
+    __shared__ UpdLds L;
     const int rb = xcd_robot();
     if (rb >= a.batch) return;
-    update_phase(a, rb, L);
-    const double* src = reinterpret_cast<const double*>(&L.prob);
-    double* dst = a.work + (size_t)rb * PROB_LEN;
-    for (int k = lane_id(); k < PROB_LEN; k += 64) dst[k] = src[k];
+    update_phase(a, rb, L.u, L.prob);
+    const double2* src = reinterpret_cast<const double2*>(&L.prob);
+    double2* dst = reinterpret_cast<double2*>(a.work + (size_t)rb * PROB_LEN);
+    for (int k = lane_id(); k < PROB_LEN / 2; k += 64) dst[k] = src[k];
 }
 
 WBC_KERNEL_ATTR void wbc_solve_kernel(KernelArgs a) {
-    __shared__ Lds L;
+    __shared__ SolveLds L;
     const int rb = xcd_robot();
     if (rb >= a.batch) return;
-    double* dst = reinterpret_cast<double*>(&L.prob);
-    const double* src = a.work + (size_t)rb * PROB_LEN;
-    for (int k = lane_id(); k < PROB_LEN; k += 64) dst[k] = src[k];
+    double2* dst = reinterpret_cast<double2*>(&L.prob);
+    const double2* src = reinterpret_cast<const double2*>(a.work + (size_t)rb * PROB_LEN);
+    for (int k = lane_id(); k < PROB_LEN / 2; k += 64) dst[k] = src[k];
     wsync();
-    solve_phase(a, rb, L);
+    solve_phase(a, rb, L.prob, L.q);
 }
 
 __global__ void wbc_reset_kernel(double* hist, const uint8_t* mask, int batch) {

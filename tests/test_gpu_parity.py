@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 import wbc_np as W
-from quadrupedwholebodycontroller_amd import DEBUG, STATELESS, Engine, split_debug, workloads
+from quadrupedwholebodycontroller_amd import DEBUG, SPLIT, STATELESS, Engine, split_debug, workloads
 
 pytestmark = pytest.mark.gpu
 
@@ -86,11 +86,14 @@ def test_update_solve_split_equals_fused():
     e = Engine(B)
     e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
     e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
-    e.step(STATELESS)
+    e.step(STATELESS)  # one fused kernel (default)
     fused = e.outputs()
     e.update(STATELESS)
     e.solve(STATELESS)
     split = e.outputs()
+    e.step(STATELESS | SPLIT)  # update kernel + solve kernel
+    step = e.outputs()
     e.close()
     for k in ("tau", "grf", "x", "status", "iters"):
         assert np.array_equal(fused[k], split[k]), k
+        assert np.array_equal(step[k], split[k]), k

@@ -22,6 +22,7 @@ for s in ${STEPS:-smoke pytest bench prof}; do
     stamps) step stamps 300 env WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_stamps.so python tools/stamps.py stance_cold 4096 ;;
     istamps) step istamps 300 env WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_istamps.so python tools/istamps.py stance_cold 4096 ;;
     stamps2) step stamps2 300 env WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_stamps.so python tools/stamps.py rl_random 8192 ;;
+    split) step split 600 python tools/split_probe.py 30 ${VARIANTS:-uw2,uw3,uw4} ;;
     variants) step variants 600 python tools/variants.py 30 ${VARIANTS:-w2,w3,w4,w5} ;;
     counters) step counters 120 rocprofv3 -L ;;
     pmc)    step pmc 1200 bash tools/pmc.sh ;;

@@ -12,7 +12,7 @@ e = Engine(B)
 e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
 e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
 for _ in range(3):
-    e.step(STATELESS)
+    e.step(STATELESS)  # the stamps live in the fused kernel
 e.synchronize()
 d = e.debug()[:, 0:6]
 out = e.outputs()

@@ -27,34 +27,43 @@ def kernel_source_hash():
     return h.hexdigest()
 
 
-def summarise(pmc_dir, kernel="wbc_step_kernel"):
-    vals = collections.defaultdict(list)
+def summarise(pmc_dir, prefix="wbc::wbc_"):
+    """Per-kernel mean of every counter over its dispatches (kernels whose name starts with prefix)."""
+    vals = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in sorted(glob.glob(os.path.join(pmc_dir, "pass*_counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
-            if kernel in r["Kernel_Name"]:
-                vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in vals.items()}, {k: len(v) for k, v in vals.items()}
+            name = r["Kernel_Name"]
+            if name.startswith(prefix):
+                short = name[len("wbc::"):].split("(")[0]
+                vals[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in vals.items()}, \
+           {k: {c: len(v) for c, v in d.items()} for k, d in vals.items()}
+
+
+def traffic_bytes(mean):
+    """HBM bytes per launch: FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE, KiB -> bytes."""
+    if "FETCH_SIZE" not in mean or "WRITE_SIZE" not in mean:
+        return None
+    return 2.0 * mean["FETCH_SIZE"] * 1024.0 + mean["WRITE_SIZE"] * 1024.0
 
 
 def main():
     pmc_dir, out = sys.argv[1], sys.argv[2]
-    kernel = sys.argv[3] if len(sys.argv) > 3 else "wbc_step_kernel"
-    workload = sys.argv[4] if len(sys.argv) > 4 else "stance_cold_b4096"
-    batch = int(sys.argv[5]) if len(sys.argv) > 5 else 4096
-    mean, n = summarise(pmc_dir, kernel)
-    rec = {"kernel": kernel, "workload": workload, "batch": batch, "dispatches": n, "per_launch": mean,
-           "kernel_source_sha256": kernel_source_hash()}
-    if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
-        rd = 2.0 * mean["FETCH_SIZE"] * 1024.0
-        wr = mean["WRITE_SIZE"] * 1024.0
-        rec["traffic_bytes_per_launch"] = rd + wr
-        rec["traffic_read_bytes"] = rd
-        rec["traffic_write_bytes"] = wr
-        rec["traffic_note"] = ("HBM bytes per launch from FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE, KiB -> B; "
-                               "separate --pmc passes with --kernel-trace only")
-    if "SQ_WAVES" in mean:
-        w = mean["SQ_WAVES"]
-        rec["per_wave"] = {k: v / w for k, v in mean.items() if k.startswith("SQ_INSTS")}
+    workload = sys.argv[3] if len(sys.argv) > 3 else "stance_cold_b4096"
+    batch = int(sys.argv[4]) if len(sys.argv) > 4 else 4096
+    step_kernels = (sys.argv[5] if len(sys.argv) > 5 else "wbc_step_kernel").split(",")
+    mean, n = summarise(pmc_dir)
+    rec = {"workload": workload, "batch": batch, "dispatches": n, "per_launch": mean,
+           "kernel_source_sha256": kernel_source_hash(),
+           "traffic_note": ("HBM bytes per launch = FETCH_SIZE x 2 (gfx950: half of wide coalesced reads counted) "
+                            "+ WRITE_SIZE, KiB -> B; separate --pmc passes with --kernel-trace only; widths other "
+                            "than 16 B/lane are uncalibrated (MI355X_MICROARCH.md)")}
+    traffic = {k: traffic_bytes(m) for k, m in mean.items()}
+    if all(traffic.get(k) is not None for k in step_kernels):
+        traffic["step"] = sum(traffic[k] for k in step_kernels)
+    rec["traffic"] = traffic
+    rec["per_wave"] = {k: {c: v / m["SQ_WAVES"] for c, v in m.items() if c.startswith("SQ_INSTS")}
+                       for k, m in mean.items() if m.get("SQ_WAVES")}
     with open(out, "w") as f:
         json.dump(rec, f, indent=1)
     print(json.dumps(rec, indent=1))

@@ -13,7 +13,7 @@ e = Engine(B)
 e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
 e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
 for _ in range(3):
-    e.step(STATELESS)
+    e.step(STATELESS)  # the stamps live in the fused kernel
 e.synchronize()
 d = e.debug()[:, DBG["STAMPS"]:DBG["STAMPS"] + 7]
 names = ["update", "qp_setup(H_s chol, x0)", "normals+C0", "GI loop", "primal recovery", "outputs"]
