@@ -227,3 +227,93 @@ def split_debug(rec):
                 Mbar_j=rec[D["MBARJ"]:D["MBARJ"] + 144].reshape(12, 12),
                 Jbar=rec[D["JBAR"]:D["JBAR"] + 216].reshape(12, 18), bbar=rec[D["BBAR"]:D["BBAR"] + 18],
                 W=rec[D["WRENCH"]:D["WRENCH"] + 6], r1=rec[D["R1"]:D["R1"] + 12], rsw=rec[D["RSW"]:D["RSW"] + 12])
+
+
+# --- batched motion planner (include/wbc_planner.h) -----------------------------------------------
+class WbcPlannerParams(C.Structure):
+    _fields_ = [(n, C.c_double) for n in ("step_length", "height_control_point", "x_offset", "y_offset",
+                                          "step_duration", "body_height", "body_initial_velocity",
+                                          "body_final_velocity", "dt")]
+
+
+PLANNER_API_SYMBOLS = ["wbc_planner_default_params", "wbc_planner_create", "wbc_planner_destroy",
+                       "wbc_planner_set_stream", "wbc_planner_set_command", "wbc_planner_reset", "wbc_planner_tick",
+                       "wbc_planner_device_outputs", "wbc_planner_get_output"]
+
+
+def _planner_lib():
+    lib = load_library()
+    if not getattr(lib, "_planner_sigs", False):
+        P, I32 = C.c_void_p, C.c_int32
+        PP = C.POINTER(P)
+        sig = {
+            "wbc_planner_default_params": ([C.POINTER(WbcPlannerParams)], I32),
+            "wbc_planner_create": ([C.POINTER(WbcPlannerParams), I32, I32, C.POINTER(P)], I32),
+            "wbc_planner_destroy": ([P], I32),
+            "wbc_planner_set_stream": ([P, P], I32),
+            "wbc_planner_set_command": ([P, P], I32),
+            "wbc_planner_reset": ([P, P], I32),
+            "wbc_planner_tick": ([P], I32),
+            "wbc_planner_device_outputs": ([P, PP, PP, PP, PP], I32),
+            "wbc_planner_get_output": ([P, P, P, P, P], I32),
+        }
+        for name, (argt, rest) in sig.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argt
+            fn.restype = rest
+        lib._planner_sigs = True
+    return lib
+
+
+class Planner:
+    """B motion planners on one GPU (wraps wbc_planner*): one tick = one plannerLoop rate.sleep()."""
+
+    def __init__(self, batch: int, device: int = 0, params: WbcPlannerParams | None = None):
+        self.lib = _planner_lib()
+        self.batch = int(batch)
+        self.h = C.c_void_p()
+        rc = self.lib.wbc_planner_create(C.byref(params) if params else None, self.batch, int(device), C.byref(self.h))
+        self._check(rc, "wbc_planner_create")
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise WbcError(f"{what} failed ({rc}): {self.lib.wbc_last_error().decode()}")
+
+    def close(self):
+        if self.h:
+            self.lib.wbc_planner_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_ptr: int):
+        self._check(self.lib.wbc_planner_set_stream(self.h, C.c_void_p(int(stream_ptr)) if stream_ptr else None),
+                    "wbc_planner_set_stream")
+
+    def set_command(self, cmd):
+        c = np.ascontiguousarray(cmd, np.float64).reshape(self.batch, 3)
+        self._check(self.lib.wbc_planner_set_command(self.h, _ptr(c)), "wbc_planner_set_command")
+
+    def reset(self, mask=None):
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8).reshape(self.batch)
+        self._check(self.lib.wbc_planner_reset(self.h, _ptr(m)), "wbc_planner_reset")
+
+    def tick(self):
+        self._check(self.lib.wbc_planner_tick(self.h), "wbc_planner_tick")
+
+    def device_outputs(self):
+        p = [C.c_void_p() for _ in range(4)]
+        self._check(self.lib.wbc_planner_device_outputs(self.h, *[C.byref(x) for x in p]), "wbc_planner_device_outputs")
+        return dict(zip(("ref", "contacts", "switching", "published"), (x.value for x in p)))
+
+    def outputs(self):
+        B = self.batch
+        ref = np.zeros((B, REF_LEN))
+        con, sw, pub = (np.zeros(B, np.uint8) for _ in range(3))
+        self._check(self.lib.wbc_planner_get_output(self.h, _ptr(ref), _ptr(con), _ptr(sw), _ptr(pub)),
+                    "wbc_planner_get_output")
+        return dict(ref=ref, contacts=con, switching=sw, published=pub)

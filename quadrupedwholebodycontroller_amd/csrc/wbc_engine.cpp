@@ -389,4 +389,7 @@ int32_t wbc_last_kernel_ms(wbc_engine* h, double* ms) {
 
 const char* wbc_last_error(void) { return g_err.c_str(); }
 
+// shared with the planner's C-ABI (wbc_planner.hip): one error string per thread for the library
+void wbc_internal_set_error(const char* msg) { g_err = msg ? msg : ""; }
+
 }  // extern "C"

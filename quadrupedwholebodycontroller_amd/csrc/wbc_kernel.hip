@@ -184,6 +184,9 @@ __device__ __forceinline__ double row0_sum(double v) {
 // robots so that robot-major rows sharing a cache line stay on one XCD.  Measured on MI355X
 // (profiles/r01/variants_xcd_remap.log): HBM traffic per launch 15.1 -> 11.4 MB but the kernel
 // 14 % slower for B = 4096 stance, so it is off by default.  Bijective for any grid size.
+#ifndef WBC_EQ_BCAST_LDS
+#define WBC_EQ_BCAST_LDS 0
+#endif
 #ifndef WBC_XCD_REMAP
 #define WBC_XCD_REMAP 0
 #endif
@@ -1200,8 +1203,21 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
                 for (int k = e; k < NQ; ++k) zp[k & 3] += cc[k] * cc[k];
                 const double zn = bcast((zp[0] + zp[1]) + (zp[2] + zp[3]), e);
                 double d[NQ];
+#if WBC_EQ_BCAST_LDS
+                // column broadcast through LDS: lane e writes rows e.., every lane reads them back
+                // (LDS instructions instead of 2 (24 - e) v_readlane on the VALU)
+                if (lane == e) {
+#pragma unroll
+                    for (int k = e & ~1; k < NQ; ++k) s.colbuf[k] = cc[k];
+                }
+                lds_sync();
+#pragma unroll
+                for (int k = 0; k < NQ; ++k) d[k] = (k >= e) ? s.colbuf[k] : 0.0;
+                lds_sync();
+#else
 #pragma unroll
                 for (int k = 0; k < NQ; ++k) d[k] = (k >= e) ? bcast(cc[k], e) : 0.0;
+#endif
                 const bool add = !(zn <= tiny * fmax(1.0, bcast(nn, e)));
                 // Householder reflection on rows e..23 (static q = e)
                 {
