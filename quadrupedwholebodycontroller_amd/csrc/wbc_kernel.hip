@@ -34,6 +34,7 @@
 namespace wbc {
 
 constexpr int NQ = 24;                  // reduced QP variables
+constexpr int C0_LANES = 52;            // max constraints: 7 ns + 24 + 6 (4 - ns) <= 52
 
 struct Frame {  // world frame of a body after stage A
     double R[9], o[3], w[3], al[3], ao[3], vo[3];
@@ -66,15 +67,18 @@ struct QpScratch {
     double L[12][13];       // Cholesky factor of the slot Hessian (row-major, lower)
     double xs[12];          // slot part of x0 = -H^-1 g
     double ild[12];         // 1 / L_kk
-    double ucon[64];
-    double colbuf[NQ];      // column broadcast (equality block)
-    double Rm[12][12];      // equality block: Rm[i][k] = R[k][i]
     union {
-        // R^-1 (upper triangular, zero elsewhere): element (i, j) at Rv[j / 2][i].{x, y}[j % 2], so
-        // lane i reads its row as 12 conflict-free ds_read_b128 and R^-1 d needs no masking
-        double2 Rv[NQ / 2][NQ];
-        double Wt[NQ][NQ];   // primal recovery: row k = u_k n_{a_k}
+        double Rm[12][12];  // equality block: Rm[i][k] = R[k][i]
+        double ucon[64];    // after the active-set loop: the primal y (24)
     };
+    double colbuf[NQ];      // column broadcast (equality block)
+    // initial constraint columns C0[:, p] = J0^T n_p (J0 = blkdiag(I, L^-T)), element k of lane p
+    // at c0[k / 2][p].{x, y}: read back on a drop (no rebuild of the normals) and used by the
+    // primal recovery (H^-1 n = J0 C0[:, p])
+    double2 c0[NQ / 2][C0_LANES];
+    // R^-1 (upper triangular, zero elsewhere): element (i, j) at Rv[j / 2][i].{x, y}[j % 2], so
+    // lane i reads its row as 12 conflict-free ds_read_b128 and R^-1 d needs no masking
+    double2 Rv[NQ / 2][NQ];
 };
 
 struct Lds {
@@ -914,80 +918,72 @@ __device__ __forceinline__ int nth_leg(int kap, int idx, int want) {
 
 // Normal n (24) and bound b of constraint p, as n^T y >= b (equalities: n^T y = b).
 // y = [qdd (12); slot l = f_l (stance) or s_l (swing), l = 0..3].
+// Branch-free over the constraint types (lanes hold different types, and divergent branches
+// would make the wave execute every type's code): each type's contribution is computed on every
+// lane and scaled by a per-lane 0 / +-1 factor (exact in fp64).
+//   R1  stance rows       Jc_j qdd + Jc_com a = r1, a = Mbar_b^-1 (Jc^T f - gw)    (cpp:494,504)
+//   R2  friction pyramid  -D_rr f_l >= 0                                          (cpp:404-424)
+//   R3  torque limits     +-(Mbar_j qdd - Jc_j^T f) >= -tau_max -+ bbar_j          (cpp:495,506,513)
+//   R4/R5 swing rows      +-(Js_j qdd + Js_com a) + s >= +-c'                     (cpp:496-497,507-515)
 __device__ void build_normal(const Prob& P, const QpMap& mp, const wbc_params& pr, int p, double* n, double& b,
                              bool& is_eq) {
-#pragma unroll
-    for (int k = 0; k < NQ; ++k) n[k] = 0.0;
-    b = 0.0;
-    is_eq = false;
-    if (p >= mp.m) return;
-    const double g0 = pr.gravity;
     const int kap = mp.kap;
-    // adds Jc_com[l,k] Mbar_b^-1 Jc_com[mm,:]^T to the stance slots (coefficient of f_mm):
-    //   delta(k,rr)/m + (d_l x e_k) . I_c^-1 (d_mm x e_rr)
-    auto slot_coupling = [&](int l, int k) {
+    const int t_fr = mp.neq, t_tq = mp.neq + mp.nfr, t_sw = t_tq + mp.ntq;
+    const bool in = p < mp.m;
+    const bool eq = in && p < t_fr;
+    const bool fr = in && p >= t_fr && p < t_tq;
+    const bool tq = in && p >= t_tq && p < t_sw;
+    const bool sw = in && p >= t_sw;
+    // per type: leg l, component k / friction face rr, row i, sign
+    int l = 0, k = 0, rr = 0;
+    double sg = 1.0;
+    if (eq) { l = nth_leg(kap, p / 3, 1); k = p % 3; }
+    if (fr) { const int q = p - t_fr; l = nth_leg(kap, q / 4, 1); rr = q % 4; }
+    if (tq) { const int q = p - t_tq; k = q / 2; sg = (q & 1) ? -1.0 : 1.0; }
+    if (sw) { const int q = p - t_sw; l = nth_leg(kap, q / 6, 0); k = (q % 6) / 2; sg = (q & 1) ? -1.0 : 1.0; }
+    const int i = tq ? k : 3 * l + k;  // Jbj / Mbj row (torque: joint index)
+    // qdd part: +-Jbj row i (R1, R4/R5) or +-Mbj row i (R3)
+    const double* row = (tq ? P.Mbj : P.Jbj) + i * 12;
+    const double sq = (eq ? 1.0 : 0.0) + ((tq || sw) ? sg : 0.0);
+#pragma unroll
+    for (int j = 0; j < 12; ++j) n[j] = sq * row[j];
+    // slot coupling through a (R1 and R4/R5): delta(k,r)/m + (d_l x e_k) . I_c^-1 (d_mm x e_r)
+    const double scp = eq ? 1.0 : (sw ? sg : 0.0);
+    double v[3];
+    {
         const double dl[3] = {P.d[3 * l], P.d[3 * l + 1], P.d[3 * l + 2]};
-        double e[3] = {k == 0 ? 1.0 : 0.0, k == 1 ? 1.0 : 0.0, k == 2 ? 1.0 : 0.0}, u[3], v[3];
+        const double e[3] = {k == 0 ? 1.0 : 0.0, k == 1 ? 1.0 : 0.0, k == 2 ? 1.0 : 0.0};
+        double u[3];
         cross3(dl, e, u);
         mv3(P.Icinv, u, v);
-#pragma unroll
-        for (int mm = 0; mm < 4; ++mm) {
-            if ((kap >> mm) & 1) {
-                const double dm[3] = {P.d[3 * mm], P.d[3 * mm + 1], P.d[3 * mm + 2]};
-                double vx[3];
-                cross3(v, dm, vx);  // (d_mm x e_rr) . v = e_rr . (v x d_mm)
-#pragma unroll
-                for (int rr = 0; rr < 3; ++rr) n[12 + 3 * mm + rr] += ((k == rr) ? P.inv_m : 0.0) + vx[rr];
-            }
-        }
-    };
-    if (p < mp.neq) {  // R1, stance rows: Jc_j qdd + Jc_com a = r1 with a = Mbar_b^-1 (Jc^T f - gw)
-        const int l = nth_leg(kap, p / 3, 1), k = p % 3, i = 3 * l + k;
-#pragma unroll
-        for (int j = 0; j < 12; ++j) n[j] = P.Jbj[i * 12 + j];
-        slot_coupling(l, k);
-        b = P.r1[i] + (k == 2 ? g0 : 0.0);
-        is_eq = true;
-    } else if (p < mp.neq + mp.nfr) {  // R2 friction pyramid (cpp:404-424): -D_rr f_l >= 0
-        const int q = p - mp.neq, l = nth_leg(kap, q / 4, 1), rr = q % 4;
-        const double nx = (rr == 0) ? -1.0 : (rr == 1 ? 1.0 : 0.0);
-        const double ny = (rr == 2) ? -1.0 : (rr == 3 ? 1.0 : 0.0);
-#pragma unroll
-        for (int ll = 0; ll < 4; ++ll) {
-            if (ll == l) {
-                n[12 + 3 * ll + 0] = nx;
-                n[12 + 3 * ll + 1] = ny;
-                n[12 + 3 * ll + 2] = pr.friction;
-            }
-        }
-    } else if (p < mp.neq + mp.nfr + mp.ntq) {  // R3 torque limits (cpp:495,506,513)
-        const int q = p - mp.neq - mp.nfr, i = q / 2;
-        const double sg = (q & 1) ? -1.0 : 1.0;
-#pragma unroll
-        for (int j = 0; j < 12; ++j) n[j] = sg * P.Mbj[i * 12 + j];
-#pragma unroll
-        for (int mm = 0; mm < 4; ++mm) {
-            if ((kap >> mm) & 1) {
-#pragma unroll
-                for (int rr = 0; rr < 3; ++rr) n[12 + 3 * mm + rr] = -sg * P.Jbj[(3 * mm + rr) * 12 + i];
-            }
-        }
-        b = (sg > 0) ? (-pr.max_torque - P.bbj[i]) : (-pr.max_torque + P.bbj[i]);
-    } else {  // R4 / R5 swing rows (cpp:496-497,507-508,514-515)
-        const int q = p - mp.neq - mp.nfr - mp.ntq, l = nth_leg(kap, q / 6, 0), k = (q % 6) / 2, i = 3 * l + k;
-        const double sg = (q & 1) ? -1.0 : 1.0;  // +: w + s >= c' (R5) ; -: -w + s >= -c' (R4)
-#pragma unroll
-        for (int j = 0; j < 12; ++j) n[j] = P.Jbj[i * 12 + j];
-        slot_coupling(l, k);
-#pragma unroll
-        for (int j = 0; j < NQ; ++j) n[j] *= sg;
-#pragma unroll
-        for (int ll = 0; ll < 4; ++ll)
-#pragma unroll
-            for (int kk = 0; kk < 3; ++kk)
-                if (ll == l && kk == k) n[12 + 3 * ll + kk] = 1.0;
-        b = sg * (P.rsw[i] + (k == 2 ? g0 : 0.0));
     }
+    // torque rows: slot of stance leg mm = -+ Jbj[3 mm + r][i] (column i)
+    const double stq = tq ? -sg : 0.0;
+#pragma unroll
+    for (int mm = 0; mm < 4; ++mm) {
+        const bool st = (kap >> mm) & 1;
+        const double dm[3] = {P.d[3 * mm], P.d[3 * mm + 1], P.d[3 * mm + 2]};
+        double vx[3];
+        cross3(v, dm, vx);  // (d_mm x e_r) . v = e_r . (v x d_mm)
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            double x = 0.0;
+            if (st) x = scp * (((k == r) ? P.inv_m : 0.0) + vx[r]) + stq * P.Jbj[(3 * mm + r) * 12 + i];
+            // friction face rr of stance leg l: (-1 | 1 | 0, 0 | 0 | -1 | 1, mu)
+            const double fv = (r == 0) ? ((rr == 0) ? -1.0 : (rr == 1 ? 1.0 : 0.0))
+                            : (r == 1) ? ((rr == 2) ? -1.0 : (rr == 3 ? 1.0 : 0.0)) : pr.friction;
+            if (fr && mm == l) x = fv;
+            if (sw && mm == l && r == k) x = 1.0;  // the slack of swing leg l
+            n[12 + 3 * mm + r] = x;
+        }
+    }
+    const double g0 = pr.gravity;
+    const double bj = P.bbj[tq ? k : 0];
+    b = 0.0;
+    if (eq) b = P.r1[i] + (k == 2 ? g0 : 0.0);
+    if (tq) b = (sg > 0) ? (-pr.max_torque - bj) : (-pr.max_torque + bj);
+    if (sw) b = sg * (P.rsw[i] + (k == 2 ? g0 : 0.0));
+    is_eq = eq;
 }
 
 // C0[:, p] = J0^T n_p with J0 = blkdiag(I12, L^-T), in place: qdd part n, slot part L^-1 n_slot
@@ -1164,6 +1160,10 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
         inrm = fast_rsq(fmax(nn, 1e-300));
         sp = sx - bp;
         to_column(s, cc);
+        if (lane < C0_LANES) {
+#pragma unroll
+            for (int k = 0; k < NQ; k += 2) s.c0[k / 2][lane] = make_double2(cc[k], cc[k + 1]);
+        }
     }
 
     zero_rinv(s);
@@ -1418,14 +1418,13 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
         }
         if (drop) {
             // C restarts from C0 and the remaining active set is re-added (rebuild mode).
-            // Opaque copy of the lane id: the constraint decode inside build_normal must not be
-            // hoisted out of the loop (LICM would keep ~40 per-lane invariants live in VGPRs).
-            double bb;
-            bool eqd;
-            int pl = lane;
-            asm volatile("" : "+v"(pl));
-            build_normal(P, mp, pr, pl, cc, bb, eqd);
-            to_column(s, cc);  // fresh C0; slacks sp are kept
+            const int pl = lane < C0_LANES ? lane : 0;
+#pragma unroll
+            for (int k = 0; k < NQ; k += 2) {  // fresh C0 (stored at the start); slacks sp are kept
+                const double2 c = s.c0[k / 2][pl];
+                cc[k] = lane < C0_LANES ? c.x : 0.0;
+                cc[k + 1] = lane < C0_LANES ? c.y : 0.0;
+            }
             zero_rinv(s);
             lds_sync();
             rbk = 0;
@@ -1435,59 +1434,37 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
     IST_FLUSH(a, rb);
 
     STAMP(a, rb, 4);
-    // primal recovery: y = x0 + H^-1 w,  w = sum_k u_k n_{a_k}  (LDS transpose-sum over active rows)
-    if (lane < 64) s.ucon[lane] = -1.0;  // slot index of constraint `lane` (or -1)
-    lds_sync();
-    if (lane < q && act >= 0) s.ucon[act] = (double)lane;
-    lds_sync();
+    // primal recovery: y = x0 + H^-1 N_A u = x0 + J0 w',  w' = sum_s u_s C0[:, a_s] (lane i < 24 forms
+    // component i from the stored initial columns); qdd part: y = w'; slots: y_s = xs + L^-T w'_s
+    double wi = 0.0;
     {
-        const int slot = is_con ? (int)s.ucon[lane] : -1;
-        const double uk = __shfl(u, slot < 0 ? 0 : slot);  // multiplier held by the slot lane
-        if (slot >= 0) {
-            double n[NQ], bb;
-            bool eqf;
-            build_normal(P, mp, pr, lane, n, bb, eqf);
-#pragma unroll
-            for (int k = 0; k < NQ; ++k) s.Wt[slot][k] = uk * n[k];
-        }
-    }
-    lds_sync();
-    double wi = 0.0;  // w_i for lane i < 24
-    if (lane < NQ) {
+        const int i = lane < NQ ? lane : 0;
         double wp[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int k = 0; k < NQ; ++k) wp[k & 3] += (k < q) ? s.Wt[k][lane] : 0.0;
-        wi = (wp[0] + wp[1]) + (wp[2] + wp[3]);
+#pragma unroll 4
+        for (int k = 0; k < q; ++k) {
+            const double uk = bcast(u, k);
+            const int ak = bcast_i(act, k);
+            const double2 c = s.c0[i >> 1][ak];
+            wp[k & 3] += uk * ((i & 1) ? c.y : c.x);
+        }
+        wi = lane < NQ ? (wp[0] + wp[1]) + (wp[2] + wp[3]) : 0.0;
     }
-    // slots: y_s = xs + L^-T L^-1 w_s (lane i < 12 handles row i of the slot block, w_s[i] = w_{12+i})
-    double ws = __shfl(wi, (lane + 12) & 63);
     double yv;
     {
-        double lrow[12], lcol[12];
+        double lcol[12];
 #pragma unroll
-        for (int k = 0; k < 12; ++k) {
-            lrow[k] = (lane < 12 && k <= lane) ? s.L[lane][k] : 1.0;
-            lcol[k] = (lane < 12 && k > lane) ? s.L[k][lane] : 0.0;
-        }
+        for (int k = 0; k < 12; ++k) lcol[k] = (lane < 12 && k > lane) ? s.L[k][lane] : 0.0;
         const double ildv = (lane < 12) ? s.ild[lane] : 1.0;
-        double zk = 0.0;
+        double zt = __shfl(wi, (lane + 12) & 63), xk_own = 0.0;  // lane k < 12: w'_{12 + k}
 #pragma unroll
-        for (int k = 0; k < 12; ++k) {
-            const double zz = bcast(ws * ildv, k);  // lane k: (w_k - sum) / L_kk
-            if (lane == k) zk = zz;
-            if (lane > k) ws -= lrow[k] * zz;
-        }
-        double zt = zk, xk_own = 0.0;
-#pragma unroll
-        for (int k = 11; k >= 0; --k) {
+        for (int k = 11; k >= 0; --k) {  // back substitution L^T x = w'_s
             const double xk = bcast(zt * ildv, k);
             if (lane == k) xk_own = xk;
             if (lane < k) zt -= lcol[k] * xk;
         }
         yv = (lane < 12) ? s.xs[lane < 12 ? lane : 0] + xk_own : 0.0;
     }
-    lds_sync();  // Wt (aliases Rinv) and ucon fully consumed
-    double* yq = s.ucon;  // y[0..23]: qdd (w[0:12]) then slots
+    double* yq = s.ucon;  // y[0..23]: qdd then slots
     if (lane < 12) { yq[lane] = wi; yq[12 + lane] = yv; }
     lds_sync();
 
