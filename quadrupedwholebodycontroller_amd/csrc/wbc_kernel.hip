@@ -64,7 +64,8 @@ struct UpdScratch {
 };
 
 struct QpScratch {
-    double L[12][13];       // Cholesky factor of the slot Hessian (row-major, lower)
+    double L[12][13];       // Cholesky factor of the slot Hessian (row-major, lower); then M = L^-1
+    __device__ double (&Mi())[12][12] { return *reinterpret_cast<double(*)[12][12]>(&L[0][0]); }
     double xs[12];          // slot part of x0 = -H^-1 g
     double ild[12];         // 1 / L_kk
     union {
@@ -987,14 +988,17 @@ __device__ void build_normal(const Prob& P, const QpMap& mp, const wbc_params& p
 }
 
 // C0[:, p] = J0^T n_p with J0 = blkdiag(I12, L^-T), in place: qdd part n, slot part L^-1 n_slot
-__device__ __forceinline__ void to_column(const QpScratch& s, double* cc) {
+__device__ __forceinline__ void to_column(QpScratch& s, double* cc) {
+    double t[12];
 #pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        double acc = cc[12 + k];
+    for (int i = 0; i < 12; ++i) {  // slot part L^-1 n_s = M n_s (M read as a broadcast)
+        double a4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int i = 0; i < k; ++i) acc -= s.L[k][i] * cc[12 + i];
-        cc[12 + k] = acc * s.ild[k];
+        for (int k = 0; k <= i; ++k) a4[k & 3] += s.Mi()[i][k] * cc[12 + k];
+        t[i] = (a4[0] + a4[1]) + (a4[2] + a4[3]);
     }
+#pragma unroll
+    for (int i = 0; i < 12; ++i) cc[12 + i] = t[i];
 }
 
 // d = C[:, p] broadcast from lane p (uniform, v_readlane)
@@ -1120,25 +1124,39 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
             for (int j = 0; j < 12; ++j) s.L[lane][j] = (j <= lane) ? hrow[j] : 0.0;
             s.ild[lane] = ildv;
         }
-        // forward substitution L z = g_s (column-oriented; z_k from lane k)
-        double zk = 0.0;
-#pragma unroll
-        for (int k = 0; k < 12; ++k) {
-            const double zz = bcast(gsv * ildv, k);  // lane k: g_k' / L_kk
-            if (lane == k) zk = zz;
-            if (lane > k) gsv -= hrow[k] * zz;
-        }
         lds_sync();  // L visible
-        // back substitution L^T x = z: lane j holds column j of L below the diagonal (L[k][j], k > j)
-        double lcol[12];
+        // M = L^-1 (lower triangular), lane j forms column j by forward substitution; every later
+        // use of the factor (C0 = L^-1 n_s, x0, primal recovery) is then a matvec without a chain
+        {
+            double m[12];
 #pragma unroll
-        for (int k = 0; k < 12; ++k) lcol[k] = (lane < 12 && k > lane) ? s.L[k][lane] : 0.0;
-        double zt = zk;
+            for (int i = 0; i < 12; ++i) {
+                double a4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int k = 11; k >= 0; --k) {
-            const double xk = bcast(zt * ildv, k);  // lane k: (z_k - sum) / L_kk
-            if (lane == k) s.xs[k] = -xk;              // x0 = -H^-1 g
-            if (lane < k) zt -= lcol[k] * xk;
+                for (int k = 0; k < i; ++k) a4[k & 3] += s.L[i][k] * m[k];
+                m[i] = (((lane == i) ? 1.0 : 0.0) - ((a4[0] + a4[1]) + (a4[2] + a4[3]))) * s.ild[i];
+            }
+            lds_sync();  // all reads of L done: M overwrites it
+            if (lane < 12) {
+#pragma unroll
+                for (int i = 0; i < 12; ++i) s.Mi()[i][lane] = (i >= lane) ? m[i] : 0.0;
+            }
+        }
+        lds_sync();
+        // x0 = -H_s^-1 g_s = -M^T (M g_s): g_k and z_k broadcast from lane k
+        {
+            double gk[12];
+#pragma unroll
+            for (int k = 0; k < 12; ++k) gk[k] = bcast(gsv, k);
+            const int i = lane < 12 ? lane : 0;
+            double z4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int k = 0; k < 12; ++k) z4[k & 3] += s.Mi()[i][k] * gk[k];
+            const double zi = (z4[0] + z4[1]) + (z4[2] + z4[3]);
+            double x4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int k = 0; k < 12; ++k) x4[k & 3] += s.Mi()[k][i] * bcast(zi, k);
+            if (lane < 12) s.xs[lane] = -((x4[0] + x4[1]) + (x4[2] + x4[3]));
         }
     }
     lds_sync();
@@ -1450,19 +1468,12 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
         wi = lane < NQ ? (wp[0] + wp[1]) + (wp[2] + wp[3]) : 0.0;
     }
     double yv;
-    {
-        double lcol[12];
+    {   // y_s = xs + M^T w'_s (lane i < 12: column i of M, w'_{12 + k} broadcast)
+        const int i = lane < 12 ? lane : 0;
+        double x4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int k = 0; k < 12; ++k) lcol[k] = (lane < 12 && k > lane) ? s.L[k][lane] : 0.0;
-        const double ildv = (lane < 12) ? s.ild[lane] : 1.0;
-        double zt = __shfl(wi, (lane + 12) & 63), xk_own = 0.0;  // lane k < 12: w'_{12 + k}
-#pragma unroll
-        for (int k = 11; k >= 0; --k) {  // back substitution L^T x = w'_s
-            const double xk = bcast(zt * ildv, k);
-            if (lane == k) xk_own = xk;
-            if (lane < k) zt -= lcol[k] * xk;
-        }
-        yv = (lane < 12) ? s.xs[lane < 12 ? lane : 0] + xk_own : 0.0;
+        for (int k = 0; k < 12; ++k) x4[k & 3] += s.Mi()[k][i] * bcast(wi, 12 + k);
+        yv = (lane < 12) ? s.xs[i] + ((x4[0] + x4[1]) + (x4[2] + x4[3])) : 0.0;
     }
     double* yq = s.ucon;  // y[0..23]: qdd then slots
     if (lane < 12) { yq[lane] = wi; yq[12 + lane] = yv; }
