@@ -103,11 +103,15 @@ enum {
 };
 
 /* Step flags. */
-#define WBC_STATELESS 1u /* cold step: history = reset values; history is neither read nor written */
+#define WBC_STATELESS 1u /* cold step: history = reset values; history is neither read nor written.
+                          * Without it the step is stateful: finite-difference history, integral
+                          * error and a QP hotstart from the previous working set (as qpOASES
+                          * SQProblem::hotstart, src/whole_body_controller.cpp:531). */
 #define WBC_DEBUG 2u     /* also write the per-robot debug record (wbc_get_debug) */
 #define WBC_NO_X 4u      /* skip the x[42] output (tau, grf, status, iters are still written) */
 #define WBC_SPLIT 8u     /* wbc_step as the update kernel + solve kernel pair instead of one fused kernel */
 #define WBC_TIMED 16u    /* wbc_step records HIP events around its kernels (wbc_last_kernel_ms) */
+#define WBC_COLD 32u     /* stateful, but the QP starts cold (no hotstart from the previous working set) */
 
 /* Debug record layout (doubles per robot), written by update/step under WBC_DEBUG. */
 enum {

@@ -102,6 +102,7 @@ wbc::KernelArgs make_args(wbc_engine* h, uint32_t flags) {
     a.batch = h->batch;
     a.stateful = (flags & WBC_STATELESS) ? 0 : 1;
     a.debug = (flags & WBC_DEBUG) ? 1 : 0;
+    a.cold = (flags & WBC_COLD) ? 1 : 0;
     return a;
 }
 }  // namespace

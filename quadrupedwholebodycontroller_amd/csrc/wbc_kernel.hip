@@ -1056,6 +1056,39 @@ __device__ __forceinline__ void add_column(QpScratch& s, int q, bool add, double
     }
 }
 
+// Multipliers and slacks of the point where every active constraint (slots 0..q-1, constraint
+// act of slot lane) holds with equality, from the slacks sp0 at the unconstrained optimum x0:
+// R^T v = -s_A (v_i = -column i of R^-1 . s_A), u = R^-1 v, s = sp0 + C[0:q]^T v.  This is the state
+// the dual method reaches by adding those constraints with full steps (used by the hotstart).
+__device__ void active_set_point(const QpScratch& s, int q, int act, double sp0, const double* cc, double& u,
+                                 double& sp) {
+    const int lane = lane_id();
+    const int i = lane < NQ ? lane : 0;
+    double a4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+        if (j < q) {
+            const int aj = bcast_i(act, j);
+            const double sa = bcast(sp0, aj < 0 ? 0 : aj);
+            const double2 r = s.Rv[i >> 1][j];  // R^-1 (j, i)
+            a4[j & 3] += ((i & 1) ? r.y : r.x) * sa;
+        }
+    }
+    const double v = (lane < q) ? -((a4[0] + a4[1]) + (a4[2] + a4[3])) : 0.0;
+    double u4[4] = {0.0, 0.0, 0.0, 0.0}, s4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+        if (j < q) {
+            const double vj = bcast(v, j);
+            const double2 r = s.Rv[j >> 1][i];  // R^-1 (i, j)
+            u4[j & 3] += ((j & 1) ? r.y : r.x) * vj;
+            s4[j & 3] += cc[j] * vj;
+        }
+    }
+    if (lane < q) u = (u4[0] + u4[1]) + (u4[2] + u4[3]);
+    sp = sp0 + ((s4[0] + s4[1]) + (s4[2] + s4[3]));
+}
+
 __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratch& s) {
     const wbc_params& pr = *a.params;
     const int lane = lane_id();
@@ -1164,10 +1197,13 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
     STAMP(a, rb, 2);
     double cc[NQ];
     double bp = 0.0, sp = 0.0, nn = 1.0, inrm = 1.0;  // |n_p|^2, 1/|n_p|
+    double sp0 = 0.0;  // slack at the unconstrained optimum x0
     bool is_eq = false, active = false;
     const bool is_con = lane < mp.m;
     {
+        EST(a, rb, 5);
         build_normal(P, mp, pr, lane, cc, bp, is_eq);
+        EST(a, rb, 6);
         double np[4] = {0.0, 0.0, 0.0, 0.0}, sq[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int k = 0; k < NQ; ++k) np[k & 3] += cc[k] * cc[k];
@@ -1177,7 +1213,10 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
         const double sx = (sq[0] + sq[1]) + (sq[2] + sq[3]);
         inrm = fast_rsq(fmax(nn, 1e-300));
         sp = sx - bp;
+        EST(a, rb, 7);
         to_column(s, cc);
+        EST(a, rb, 8);
+        sp0 = sp;
         if (lane < C0_LANES) {
 #pragma unroll
             for (int k = 0; k < NQ; k += 2) s.c0[k / 2][lane] = make_double2(cc[k], cc[k + 1]);
@@ -1337,13 +1376,68 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
         lds_sync();
     }
     EST(a, rb, 4);
+
+    // Hotstart (qpOASES SQProblem::hotstart, cpp:523-535): in stateful mode, the inequalities that
+    // were active at the end of the previous solve (same contact mask) are re-added as a block
+    // (the loop's rebuild mode), then multipliers and slacks are set in closed form.  If any
+    // re-added multiplier comes out negative, the warm set is dropped and the solve restarts
+    // from the equality-constrained point, as a cold solve would.
+    double* Hh = a.stateful ? a.hist + (size_t)rb * HIST_LEN : nullptr;
+    int warm_phase = 0;  // 1: re-adding the warm set, 2: re-adding the equalities after rejecting it
+    bool warm_fail = false;
+    if (!done && Hh && !a.cold) {
+        const unsigned long long ws = (unsigned long long)(unsigned)Hh[H_WSLO] |
+                                      ((unsigned long long)(unsigned)Hh[H_WSHI] << 32);
+        unsigned long long wm = ((int)Hh[H_WSKAP] == kap) ? ws : 0ull;
+        wm &= ~((1ull << mp.neq) - 1ull);                        // inequalities only
+        wm &= (mp.m >= 64) ? ~0ull : ((1ull << mp.m) - 1ull);
+        const int nw = __popcll(wm);
+        if (nw > 0 && neq_added + nw <= NQ) {
+            const bool mine = (wm >> lane) & 1ull;
+            const int slot = neq_added + __popcll(wm & ((1ull << lane) - 1ull));
+            if (mine) s.colbuf[slot] = (double)lane;
+            lds_sync();
+            if (lane >= neq_added && lane < neq_added + nw) act = (int)s.colbuf[lane];
+            if (mine) active = true;
+            lds_sync();
+            rbk = neq_added;
+            q = neq_added + nw;
+            warm_phase = 1;
+        }
+    }
     IST_DECL;
 
     while (!done) {
         // compiler barrier: LDS reads of the problem (build_normal / to_column on the rare drop
         // path) stay inside the loop instead of being hoisted into registers for its whole length
         asm volatile("" ::: "memory");
-        if (rbk >= q) rbk = -1;  // rebuild finished
+        if (rbk >= q) {  // rebuild finished
+            rbk = -1;
+            if (warm_phase) {
+                active_set_point(s, q, act, sp0, cc, u, sp);
+                const bool neg = lane >= neq_added && lane < q && u < -1e-10;
+                if (warm_phase == 1 && (warm_fail || wave_any(neg))) {
+                    // reject the warm set: back to the equality slots, rebuilt from C0
+                    const int pl = lane < C0_LANES ? lane : 0;
+#pragma unroll
+                    for (int k = 0; k < NQ; k += 2) {
+                        const double2 c = s.c0[k / 2][pl];
+                        cc[k] = lane < C0_LANES ? c.x : 0.0;
+                        cc[k + 1] = lane < C0_LANES ? c.y : 0.0;
+                    }
+                    zero_rinv(s);
+                    lds_sync();
+                    if (lane >= neq_added) { act = -1; u = 0.0; }
+                    if (!is_eq) active = false;
+                    q = neq_added;
+                    rbk = 0;
+                    warm_phase = 2;
+                    continue;
+                }
+                if (lane >= neq_added && lane < q && u < 0.0) u = 0.0;
+                warm_phase = 0;
+            }
+        }
         const bool rebuild = rbk >= 0;
         int col, pos;
         if (rebuild) {
@@ -1385,6 +1479,11 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
 
         // step (skipped in rebuild mode: the active set is re-added as is)
         bool add = true, drop = false;
+        if (rebuild && warm_phase == 1 && !(zn > tiny * fmax(1.0, bcast(nn, col)))) {
+            add = false;  // a warm constraint dependent on the others: reject the warm set
+            warm_fail = true;
+            ++rbk;
+        }
         if (!rebuild) {
             const double sps = bcast(sp, pstar);
             // partial step: keep active inequality multipliers >= 0
@@ -1527,6 +1626,14 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
     if (lane == 0) {
         a.status[rb] = status;
         a.iters[rb] = iters;
+    }
+    if (Hh) {  // working set for the next cycle's hotstart
+        const unsigned long long am = __ballot(is_con && !is_eq && active);
+        if (lane == 0) {
+            Hh[H_WSLO] = ok ? (double)(unsigned)(am & 0xffffffffull) : 0.0;
+            Hh[H_WSHI] = ok ? (double)(unsigned)(am >> 32) : 0.0;
+            Hh[H_WSKAP] = (double)kap;
+        }
     }
 }
 

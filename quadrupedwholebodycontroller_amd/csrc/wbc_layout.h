@@ -9,8 +9,9 @@ namespace wbc {
 // Per-robot history that survives between control cycles (stateful mode).  Compact form of
 // the reference's finite-difference state (hpp:154-161): T_old (top rows only vary:
 // [Ad^-1(r_old), Mbar_b^-1 A_j]), Jbar_old (com part [I, -S(p_f - c)] from d_old, joint part),
-// Tdot_inv (top 6 rows), integralError_, the contacts of Jbar_old, and a valid flag
-// (0 right after setInitialState: T_old = I, J_old = 0, Tdot_inv = 0, cpp:84-104).
+// Tdot_inv (top 6 rows), integralError_, the contacts of Jbar_old, a valid flag
+// (0 right after setInitialState: T_old = I, J_old = 0, Tdot_inv = 0, cpp:84-104), and the
+// working set of the previous QP (qpOASES SQProblem::hotstart, cpp:531).
 enum HistOff {
     H_ROLD = 0,     // r_old = c - p_B of the previous cycle (3)
     H_MAOLD = 3,    // Mbar_b^-1 A_j of the previous cycle, 6x12 row-major (72)
@@ -20,7 +21,10 @@ enum HistOff {
     H_EINT = 339,   // integralError_ (6)
     H_KOLD = 345,   // contact bitmask of the previous cycle (as double)
     H_VALID = 346,  // 0 after reset
-    HIST_LEN = 348
+    H_WSLO = 347,   // active inequality set of the previous solve, lanes 0..31 (bitmask as double)
+    H_WSHI = 348,   //   lanes 32..63
+    H_WSKAP = 349,  // contact mask that active set belongs to (hotstart only for the same mask)
+    HIST_LEN = 350
 };
 
 // Assembled per-robot problem: written by the update phase, read by the solve phase
@@ -63,6 +67,7 @@ struct KernelArgs {
     int32_t batch;
     int32_t stateful;   // read / write history
     int32_t debug;      // write debug records
+    int32_t cold;       // stateful, but no QP hotstart (WBC_COLD)
 };
 
 

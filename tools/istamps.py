@@ -32,3 +32,7 @@ q = e.debug()[:, 20:25]
 qn = ["eq fast path (Householder)", "eq generic path", "R/s to LDS + substitutions", "u, R^-1 rows, slacks"]
 dq = np.diff(q, axis=1)
 print(json.dumps({n: float(np.median(dq[:, i])) for i, n in enumerate(qn)}, indent=1))
+n = e.debug()[:, 25:29]
+nn = ["build_normal", "norms", "to_column"]
+dn = np.diff(n, axis=1)
+print(json.dumps({k: float(np.median(dn[:, i])) for i, k in enumerate(nn)}, indent=1))
