@@ -140,6 +140,14 @@ typedef struct wbc_engine wbc_engine;
 /* Defaults of config/params_controller.yaml and the lumped reference URDF. */
 int32_t wbc_default_params(wbc_params* out);
 int32_t wbc_anymal_model(wbc_model* out);
+/* Model from a URDF file at run time (replaces ModelLoader::loadModelFromFile +
+ * KinDynComputations::loadRobotModel, cpp:26-40, and the getFrameIndex lookups, cpp:327-379): any
+ * 12-DoF quadruped whose legs are 3-revolute-joint chains off the floating base.  Fixed joints are
+ * lumped into their parent bodies (exact for M, C nu and frame kinematics).  legs: the 4 leg name
+ * prefixes in model order (NULL = LH, LF, RF, RH); joints: the 3 joint suffixes from the base out
+ * (NULL = HAA, HFE, KFE), joint names <leg>_<suffix>; foot frames <leg>_<foot_suffix> (NULL = FOOT). */
+int32_t wbc_model_from_urdf(const char* urdf_path, const char* const* legs, const char* const* joints,
+                            const char* foot_suffix, wbc_model* out);
 
 int32_t wbc_create(const wbc_model* model, const wbc_params* params, int32_t batch, int32_t device,
                    wbc_engine** out);

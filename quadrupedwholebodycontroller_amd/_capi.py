@@ -27,7 +27,7 @@ C_API_SYMBOLS = [
     "wbc_default_params", "wbc_anymal_model", "wbc_create", "wbc_destroy", "wbc_batch", "wbc_set_stream",
     "wbc_set_state", "wbc_set_reference", "wbc_bind_device_inputs", "wbc_bind_device_outputs", "wbc_reset", "wbc_update", "wbc_solve",
     "wbc_step", "wbc_synchronize", "wbc_get_output", "wbc_device_outputs", "wbc_get_debug", "wbc_last_kernel_ms",
-    "wbc_last_error",
+    "wbc_last_error", "wbc_model_from_urdf",
 ]
 
 
@@ -91,6 +91,7 @@ def load_library(path: str = LIB_PATH):
         "wbc_get_debug": ([P, P], I32),
         "wbc_last_kernel_ms": ([P, dp], I32),
         "wbc_last_error": ([], C.c_char_p),
+        "wbc_model_from_urdf": ([C.c_char_p, P, P, C.c_char_p, C.POINTER(WbcModel)], I32),
     }
     for name, (argt, rest) in sig.items():
         fn = getattr(lib, name)
@@ -108,6 +109,25 @@ def default_params() -> WbcParams:
     p = WbcParams()
     load_library().wbc_default_params(C.byref(p))
     return p
+
+
+def model_from_urdf(path: str, legs=None, joints=None, foot_suffix=None) -> WbcModel:
+    """wbc_model_from_urdf: lumped 12-DoF quadruped model from a URDF file (raises WbcError)."""
+    lib = load_library()
+
+    def names(v):
+        if v is None:
+            return None
+        arr = (C.c_char_p * len(v))(*[x.encode() for x in v])
+        return C.cast(arr, C.c_void_p), arr
+
+    m = WbcModel()
+    lg, jn = names(legs), names(joints)
+    rc = lib.wbc_model_from_urdf(path.encode(), lg[0] if lg else None, jn[0] if jn else None,
+                                 foot_suffix.encode() if foot_suffix else None, C.byref(m))
+    if rc != 0:
+        raise WbcError(f"wbc_model_from_urdf failed ({rc}): {lib.wbc_last_error().decode()}")
+    return m
 
 
 def anymal_model() -> WbcModel:

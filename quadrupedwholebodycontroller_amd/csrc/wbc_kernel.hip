@@ -1065,7 +1065,6 @@ __device__ void active_set_point(const QpScratch& s, int q, int act, double sp0,
     const int lane = lane_id();
     const int i = lane < NQ ? lane : 0;
     double a4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
     for (int j = 0; j < NQ; ++j) {
         if (j < q) {
             const int aj = bcast_i(act, j);
@@ -1076,7 +1075,6 @@ __device__ void active_set_point(const QpScratch& s, int q, int act, double sp0,
     }
     const double v = (lane < q) ? -((a4[0] + a4[1]) + (a4[2] + a4[3])) : 0.0;
     double u4[4] = {0.0, 0.0, 0.0, 0.0}, s4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
     for (int j = 0; j < NQ; ++j) {
         if (j < q) {
             const double vj = bcast(v, j);
@@ -1556,15 +1554,16 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
     double wi = 0.0;
     {
         const int i = lane < NQ ? lane : 0;
-        double wp[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
-        for (int k = 0; k < q; ++k) {
-            const double uk = bcast(u, k);
-            const int ak = bcast_i(act, k);
-            const double2 c = s.c0[i >> 1][ak];
-            wp[k & 3] += uk * ((i & 1) ? c.y : c.x);
+        double w0 = 0.0, w1 = 0.0;  // two chains (even / odd slots)
+        for (int k = 0; k < q; k += 2) {
+            const double2 c = s.c0[i >> 1][bcast_i(act, k)];
+            w0 += bcast(u, k) * ((i & 1) ? c.y : c.x);
+            if (k + 1 < q) {
+                const double2 c1 = s.c0[i >> 1][bcast_i(act, k + 1)];
+                w1 += bcast(u, k + 1) * ((i & 1) ? c1.y : c1.x);
+            }
         }
-        wi = lane < NQ ? (wp[0] + wp[1]) + (wp[2] + wp[3]) : 0.0;
+        wi = lane < NQ ? w0 + w1 : 0.0;
     }
     double yv;
     {   // y_s = xs + M^T w'_s (lane i < 12: column i of M, w'_{12 + k} broadcast)

@@ -100,13 +100,13 @@ def load_urdf(path):
     return links, joints
 
 
-def build(links, joints, leg_order=LEG_ORDER):
+def build(links, joints, leg_order=LEG_ORDER, joint_suffix=JOINT_SUFFIX, foot_suffix="FOOT"):
     children = {}
     for name, j in joints.items():
         children.setdefault(j["parent"], []).append(name)
     parents = {j["child"] for j in joints.values()}
     roots = [l for l in links if l not in parents]
-    assert roots == ["base"], roots
+    assert len(roots) == 1, roots
 
     def lump(link):
         """Collect the rigid cluster rooted at `link`: its inertial, the revolute joints that
@@ -128,13 +128,13 @@ def build(links, joints, leg_order=LEG_ORDER):
                     out_joints.append((jn, Rc, pc))
         return inert, out_joints, frames
 
-    base_inert, base_out, _ = lump("base")
+    base_inert, base_out, _ = lump(roots[0])
     out_by_name = {jn: (Rc, pc) for jn, Rc, pc in base_out}
     model = dict(base=dict(mass=base_inert.m, com=base_inert.c.tolist(), inertia=base_inert.I.tolist()),
                  legs=[], leg_order=list(leg_order), joint_names=[], foot_names=[])
     total = base_inert.m
     for leg in leg_order:
-        jn = f"{leg}_{JOINT_SUFFIX[0]}"
+        jn = f"{leg}_{joint_suffix[0]}"
         Rc, pc = out_by_name[jn]
         leg_links = []
         for k in range(3):
@@ -146,13 +146,13 @@ def build(links, joints, leg_order=LEG_ORDER):
                                   body=j["child"]))
             model["joint_names"].append(jn)
             if k < 2:
-                nxt = f"{leg}_{JOINT_SUFFIX[k + 1]}"
+                nxt = f"{leg}_{joint_suffix[k + 1]}"
                 match = [o for o in outs if o[0] == nxt]
                 assert len(match) == 1, (nxt, [o[0] for o in outs])
                 jn, Rc, pc = match[0]
             else:
                 assert not outs
-                foot = f"{leg}_FOOT"
+                foot = f"{leg}_{foot_suffix}"
                 model["foot_names"].append(foot)
                 model.setdefault("foot", []).append(frames[foot][1].tolist())
         model["legs"].append(leg_links)
