@@ -22,6 +22,7 @@
 #define WBC_CONTROLLER_HPP
 
 #include <array>
+#include <cstdint>
 #include <functional>
 #include <string>
 #include <vector>
@@ -35,8 +36,26 @@ constexpr int numberOfLegs = WBC_NUM_LEGS;
 constexpr int qpNumberOfVariables = WBC_NV;
 
 // std_msgs/Float64MultiArray, gazebo_msgs/ModelStates, sensor_msgs/JointState, anymal_wbc/WbcReferenceMsg
+// (all fields of the ROS messages, so include/wbc_ros_wire.hpp round-trips their wire bytes)
+struct MultiArrayDimension {
+    std::string label;
+    uint32_t size = 0, stride = 0;
+};
+struct MultiArrayLayout {
+    std::vector<MultiArrayDimension> dim;
+    uint32_t data_offset = 0;
+};
 struct Float64MultiArray {
+    MultiArrayLayout layout;  // left empty by the reference (cpp:558-576)
     std::vector<double> data;
+};
+struct Time {
+    uint32_t sec = 0, nsec = 0;
+};
+struct Header {
+    uint32_t seq = 0;
+    Time stamp;
+    std::string frame_id;
 };
 struct Vector3 {
     double x = 0, y = 0, z = 0;
@@ -57,6 +76,7 @@ struct ModelStates {
     std::vector<Twist> twist;
 };
 struct JointState {
+    Header header;
     std::vector<std::string> name;
     std::vector<double> position, velocity, effort;
 };
