@@ -112,6 +112,7 @@ enum {
 #define WBC_SPLIT 8u     /* wbc_step as the update kernel + solve kernel pair instead of one fused kernel */
 #define WBC_TIMED 16u    /* wbc_step records HIP events around its kernels (wbc_last_kernel_ms) */
 #define WBC_COLD 32u     /* stateful, but the QP starts cold (no hotstart from the previous working set) */
+#define WBC_FUSED 64u    /* wbc_step as the single fused kernel (the build's default form may be the pair) */
 
 /* Debug record layout (doubles per robot), written by update/step under WBC_DEBUG. */
 enum {

@@ -10,9 +10,9 @@ behind the C-ABI in include/wbc.h.  This package is the Python view of that C-AB
 
 The product path has no CPU fallback: without libwbc_hip.so or a GPU it raises.
 """
-from ._capi import (COLD, DEBUG, NO_X, SPLIT, STATELESS, TIMED, QP_INFEASIBLE, QP_MAX_ITER, QP_NUMERIC, QP_OK, Engine, WbcError,  # noqa: F401
+from ._capi import (COLD, DEBUG, FUSED, NO_X, SPLIT, STATELESS, TIMED, QP_INFEASIBLE, QP_MAX_ITER, QP_NUMERIC, QP_OK, Engine, WbcError,  # noqa: F401
                     WbcModel, WbcParams, anymal_model, default_params, load_library, model_from_urdf, split_debug, Planner,
                     WbcPlannerParams)
 
 __all__ = ["Engine", "Planner", "WbcPlannerParams", "model_from_urdf", "WbcError", "WbcModel", "WbcParams", "anymal_model", "default_params", "load_library",
-           "split_debug", "STATELESS", "DEBUG", "NO_X", "SPLIT", "TIMED", "COLD", "QP_OK", "QP_MAX_ITER", "QP_INFEASIBLE", "QP_NUMERIC"]
+           "split_debug", "STATELESS", "DEBUG", "NO_X", "SPLIT", "TIMED", "COLD", "FUSED", "QP_OK", "QP_MAX_ITER", "QP_INFEASIBLE", "QP_NUMERIC"]

@@ -16,6 +16,7 @@
 extern "C" hipError_t wbc_launch_step(const wbc::KernelArgs* a, hipStream_t st);
 extern "C" hipError_t wbc_launch_update(const wbc::KernelArgs* a, hipStream_t st);
 extern "C" hipError_t wbc_launch_solve(const wbc::KernelArgs* a, hipStream_t st);
+extern "C" int wbc_kernel_default_split();
 extern "C" hipError_t wbc_launch_reset(double* hist, const uint8_t* mask, int batch, hipStream_t st);
 
 namespace {
@@ -324,7 +325,9 @@ int32_t wbc_step(wbc_engine* h, uint32_t flags) {
     wbc::KernelArgs a = make_args(h, flags);
     const bool timed = (flags & WBC_TIMED) != 0;  // event packets cost a few us between kernels
     if (timed) WBC_HIP(hipEventRecord(h->ev0, h->stream));
-    if (flags & WBC_SPLIT) {  // measured ~5 % slower than fused at B = 4096 (profiles/r01/)
+    // default form chosen at build time (WBC_DEFAULT_SPLIT, by measurement); the flags force one
+    const bool split = (flags & WBC_SPLIT) || (!(flags & WBC_FUSED) && wbc_kernel_default_split());
+    if (split) {
         WBC_HIP(wbc_launch_update(&a, h->stream));
         WBC_HIP(wbc_launch_solve(&a, h->stream));
     } else {

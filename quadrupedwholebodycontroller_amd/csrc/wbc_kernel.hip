@@ -61,6 +61,7 @@ struct UpdScratch {
     double Mjj[12][3];      // leg block rows of M
     double hj[12];          // joint bias (C nu)_j
     double cen[40];         // uniform scratch (CEN_*)
+    double yv[6];           // Tdot_inv nu exchange (segmented update kernel)
 };
 
 struct QpScratch {
@@ -109,6 +110,15 @@ __device__ __forceinline__ double bcast(double v, int lane) {
     return __hiloint2double(hi, lo);
 }
 __device__ __forceinline__ int bcast_i(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+// Broadcast into VGPRs through the LDS crossbar (ds_bpermute; no LDS memory): the result is not
+// known to be uniform, so it stays out of the SGPR file (readlane results are SGPRs, and a
+// 24-vector of them overflows it into spill code)
+__device__ __forceinline__ double vbcast(double v, int lane) {
+    const int addr = lane << 2;
+    const int lo = __builtin_amdgcn_ds_bpermute(addr, __double2loint(v));
+    const int hi = __builtin_amdgcn_ds_bpermute(addr, __double2hiint(v));
+    return __hiloint2double(hi, lo);
+}
 
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double v) {
@@ -184,6 +194,40 @@ __device__ __forceinline__ double row0_sum(double v) {
     return bcast(v, 0);
 }
 
+// Segmented forms for the update kernel with several robots per wave (SUB lanes per robot, SUB in
+// {16, 32, 64}): the row sum above, then the segment head's value to every lane of the segment
+// (v_readlane for 64; ds_swizzle bitmask mode, lane & 0x10 or lane & 0 within each 32-lane half,
+// for 16 and 32), so every lane of a robot holds the same bits.
+template <int AND>
+__device__ __forceinline__ double swz_head(double v) {
+    const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), AND);
+    const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), AND);
+    return __hiloint2double(hi, lo);
+}
+template <int SUB>
+__device__ __forceinline__ double seg_sum(double v) {
+    static_assert(SUB == 16 || SUB == 32 || SUB == 64, "segment width");
+    if constexpr (SUB == 64) {
+        return row0_sum(v);
+    } else {
+        v += dpp_d<0x128>(v);
+        v += dpp_d<0x124>(v);
+        v += dpp_d<0x122>(v);
+        v += dpp_d<0x121>(v);
+        return swz_head<SUB == 16 ? 0x10 : 0x00>(v);
+    }
+}
+template <int SUB>
+__device__ __forceinline__ bool seg_any(bool p) {
+    if constexpr (SUB == 64) {
+        return __any(p);
+    } else {
+        const unsigned long long m = __ballot(p);
+        const int seg = (int)threadIdx.x / SUB;
+        return ((m >> (seg * SUB)) & ((1ull << SUB) - 1ull)) != 0ull;
+    }
+}
+
 // XCD-aware robot index (optional, -DWBC_XCD_REMAP=1).  Workgroups are dealt round-robin to the
 // 8 XCDs (blockIdx % 8), each with its own L2; the remap gives every XCD a contiguous range of
 // robots so that robot-major rows sharing a cache line stay on one XCD.  Measured on MI355X
@@ -191,6 +235,12 @@ __device__ __forceinline__ double row0_sum(double v) {
 // 14 % slower for B = 4096 stance, so it is off by default.  Bijective for any grid size.
 #ifndef WBC_EQ_BCAST_LDS
 #define WBC_EQ_BCAST_LDS 0
+#endif
+#ifndef WBC_EQ_BPERM
+#define WBC_EQ_BPERM 0
+#endif
+#ifndef WBC_LOOP_BPERM
+#define WBC_LOOP_BPERM 0
 #endif
 #ifndef WBC_XCD_REMAP
 #define WBC_XCD_REMAP 0
@@ -336,10 +386,13 @@ __device__ __forceinline__ double sel3(const double* v, int k) { return k == 0 ?
 // update phase (≙ updateState, cpp:256-294, plus the per-cycle terms of solveQP that do not
 // depend on the QP: computeDesiredWrench cpp:426-445, swing commands cpp:447-464, bounds cpp:503-515)
 // ---------------------------------------------------------------------------------------
-__device__ void update_phase(const KernelArgs& a, int rb, UpdScratch& s, Prob& P) {
+// SUB = lanes per robot (64: one robot per wave; 16 / 32: 4 / 2 robots per wave, each with its
+// own scratch); lane = lane within the robot's segment; wr = false for a padding segment past the
+// batch (computes a duplicate robot, writes nothing to HBM).
+template <int SUB>
+__device__ void update_phase(const KernelArgs& a, int rb, int lane, bool wr, UpdScratch& s, Prob& P) {
     const wbc_model& md = *a.model;
     const wbc_params& pr = *a.params;
-    const int lane = lane_id();
     const int kap = a.contacts[rb];
     const bool switching = a.switching[rb] != 0;
     const bool stateful = a.stateful != 0;
@@ -348,7 +401,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, UpdScratch& s, Prob& P
     UST(a, rb, 0);
 
     // inputs, one element per lane (robot-major arrays -> contiguous per wave); sin/cos per joint
-    {
+    if constexpr (SUB == 64) {
         // both loads issued before either is used: lane k < 64 reads input k, lanes 0..26 also
         // read input 64 + k (all in the reference block)
         const double* p0 = (lane < 7) ? a.base_pose + (size_t)rb * 7 + lane
@@ -369,6 +422,29 @@ __device__ void update_phase(const KernelArgs& a, int rb, UpdScratch& s, Prob& P
             s.sc[lane - 25][1] = cs;
         }
         const bool anybad = wave_any(bad);
+        if (lane == 0) { P.flags = anybad ? 1.0 : 0.0; P.kappa = (double)kap; }
+    } else {
+        bool bad = false;
+#pragma unroll
+        for (int it = 0; it < (91 + SUB - 1) / SUB; ++it) {
+            const int k = lane + it * SUB;
+            if (k < 91) {
+                const double* p = (k < 7) ? a.base_pose + (size_t)rb * 7 + k
+                                : (k < 25) ? a.nu + (size_t)rb * 18 + (k - 7)
+                                : (k < 37) ? a.qj + (size_t)rb * 12 + (k - 25)
+                                           : a.ref + (size_t)rb * 54 + (k - 37);
+                const double v = *p;
+                bad = bad || !isfinite(v);
+                s.in[k] = v;
+            }
+        }
+        if (lane < 12) {
+            double sn, cs;
+            sincos(a.qj[(size_t)rb * 12 + lane], &sn, &cs);
+            s.sc[lane][0] = sn;
+            s.sc[lane][1] = cs;
+        }
+        const bool anybad = seg_any<SUB>(bad);
         if (lane == 0) { P.flags = anybad ? 1.0 : 0.0; P.kappa = (double)kap; }
     }
     wsync();
@@ -498,8 +574,8 @@ __device__ void update_phase(const KernelArgs& a, int rb, UpdScratch& s, Prob& P
         // mass-weighted sums over the 13 bodies (lanes >= 13 hold mb = 0)
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            cd[i] = row0_sum(mb * vc[i]);
-            c[i] = row0_sum(mb * cb[i]);
+            cd[i] = seg_sum<SUB>(mb * vc[i]);
+            c[i] = seg_sum<SUB>(mb * cb[i]);
         }
     }
     wsync();
@@ -538,7 +614,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, UpdScratch& s, Prob& P
             t[5] = bd.I[5] - mb * d[1] * d[2];
         }
 #pragma unroll
-        for (int k = 0; k < 6; ++k) t[k] = row0_sum(t[k]);
+        for (int k = 0; k < 6; ++k) t[k] = seg_sum<SUB>(t[k]);
         Ic[0] = t[0]; Ic[4] = t[1]; Ic[8] = t[2];
         Ic[1] = Ic[3] = t[3]; Ic[2] = Ic[6] = t[4]; Ic[5] = Ic[7] = t[5];
         inv3(Ic, Icinv);
@@ -553,7 +629,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, UpdScratch& s, Prob& P
             for (int i = 0; i < 3; ++i) { hb[i] = bd.F[i]; hb[3 + i] = t[i] + bd.N[i]; }
         }
 #pragma unroll
-        for (int k = 0; k < 6; ++k) hb[k] = row0_sum(hb[k]);
+        for (int k = 0; k < 6; ++k) hb[k] = seg_sum<SUB>(hb[k]);
     }
     UST(a, rb, 5);
     // stage C: per joint: centroidal momentum column (about c), leg block of M, joint bias (C nu)_j
@@ -618,8 +694,15 @@ __device__ void update_phase(const KernelArgs& a, int rb, UpdScratch& s, Prob& P
 #pragma unroll
                 for (int cc = 0; cc < 18; ++cc) yl += H[H_TDINV + lane * 18 + cc] * s.in[7 + cc];
             }
+            if constexpr (SUB == 64) {
 #pragma unroll
-            for (int k = 0; k < 6; ++k) y[k] = bcast(yl, k);
+                for (int k = 0; k < 6; ++k) y[k] = bcast(yl, k);
+            } else {
+                if (lane < 6) s.yv[lane] = yl;
+                wsync();
+#pragma unroll
+                for (int k = 0; k < 6; ++k) y[k] = s.yv[k];
+            }
         }
     }
     // h' = C nu + M[:, 0:6] y ; M_bb = [[m I, -m S(r)], [m S(r), I_c - m S(r)^2]] ; zeta = Mbar_b^-1 Ad^T h'_b
@@ -698,19 +781,27 @@ __device__ void update_phase(const KernelArgs& a, int rb, UpdScratch& s, Prob& P
     }
     UST(a, rb, 8);
     // T_top = [Ad^-1(r), Mbar_b^-1 A_j]; Tdot_inv for the next cycle (cpp:291-293)
-    double tcol[6] = {0, 0, 0, 0, 0, 0};
+    constexpr int NT = (18 + SUB - 1) / SUB;  // Tdot_inv columns per lane
+    double tcol[NT][6];
+#pragma unroll
+    for (int it = 0; it < NT; ++it)
+#pragma unroll
+        for (int q = 0; q < 6; ++q) tcol[it][q] = 0.0;
     if (stateful) {
         double dr[3] = {0, 0, 0};
         if (!switching) {
 #pragma unroll
             for (int i = 0; i < 3; ++i) dr[i] = (r[i] - H[H_ROLD + i]) / dt;
         }
-        if (lane >= 3 && lane < 6) {  // lin rows, cols 3..5: S(dr)
-            const int cc = lane - 3;
+#pragma unroll
+        for (int it = 0; it < NT; ++it) {
+        const int ln = lane + it * SUB;
+        if (ln >= 3 && ln < 6) {  // lin rows, cols 3..5: S(dr)
+            const int cc = ln - 3;
             double e[3] = {cc == 0 ? 1.0 : 0.0, cc == 1 ? 1.0 : 0.0, cc == 2 ? 1.0 : 0.0};
-            cross3(dr, e, tcol);
-        } else if (lane >= 6 && lane < 18) {
-            const int j = lane - 6;
+            cross3(dr, e, tcol[it]);
+        } else if (ln >= 6 && ln < 18) {
+            const int j = ln - 6;
             double Tj[6];
 #pragma unroll
             for (int rr = 0; rr < 3; ++rr) {
@@ -722,16 +813,21 @@ __device__ void update_phase(const KernelArgs& a, int rb, UpdScratch& s, Prob& P
             cross3(r, &Tj[3], t2);
 #pragma unroll
             for (int rr = 0; rr < 3; ++rr) {
-                tcol[rr] = -(t1[rr] + Tj[rr] + t2[rr]);
-                tcol[3 + rr] = -Tj[3 + rr];
+                tcol[it][rr] = -(t1[rr] + Tj[rr] + t2[rr]);
+                tcol[it][3 + rr] = -Tj[3 + rr];
             }
+        }
         }
     }
     wsync();  // all reads of the old history done
-    if (stateful) {
-        if (lane < 18) {
+    if (stateful && wr) {
 #pragma unroll
-            for (int rr = 0; rr < 6; ++rr) H[H_TDINV + rr * 18 + lane] = tcol[rr];
+        for (int it = 0; it < NT; ++it) {
+            const int ln = lane + it * SUB;
+            if (ln < 18) {
+#pragma unroll
+                for (int rr = 0; rr < 6; ++rr) H[H_TDINV + rr * 18 + ln] = tcol[it][rr];
+            }
         }
         if (lane < 12) {
             const int j = lane;
@@ -784,17 +880,17 @@ __device__ void update_phase(const KernelArgs& a, int rb, UpdScratch& s, Prob& P
         const double e = s.cen[CEN_POSE + k] - ref[k];
         P.W[k] = -kp * e - pr.kd * (s.cen[CEN_VC + k] - ref[6 + k]) - pr.ki * eint +
                  (k == 2 ? md.total_mass * pr.gravity : 0.0) + mba;
-        if (stateful) H[H_EINT + k] = eint + e / pr.loop_rate;
+        if (stateful && wr) H[H_EINT + k] = eint + e / pr.loop_rate;
     }
     wsync();
-    if (stateful) {
-        for (int k = lane; k < 144; k += 64) H[H_JBJOLD + k] = P.Jbj[k];
+    if (stateful && wr) {
+        for (int k = lane; k < 144; k += SUB) H[H_JBJOLD + k] = P.Jbj[k];
         if (lane < 12) H[H_DOLD + lane] = P.d[lane];
         if (lane < 3) H[H_ROLD + lane] = s.cen[CEN_R + lane];
         if (lane == 0) { H[H_KOLD] = (double)kap; H[H_VALID] = 1.0; }
     }
     UST(a, rb, 10);
-    if (debug) {
+    if (debug && wr) {
         double* D = a.dbg + (size_t)rb * WBC_DBG_LEN;
         if (lane < 3) {
             D[WBC_DBG_COM + lane] = s.cen[CEN_C + lane];
@@ -815,7 +911,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, UpdScratch& s, Prob& P
             if (aa == 1) return bb == 0 ? r[2] : -r[0];
             return bb == 0 ? -r[1] : r[0];
         };
-        for (int e = lane; e < 324; e += 64) {
+        for (int e = lane; e < 324; e += SUB) {
             const int i = e / 18, j = e % 18;
             double v;
             if (i < 6 && j < 6) {
@@ -840,14 +936,14 @@ __device__ void update_phase(const KernelArgs& a, int rb, UpdScratch& s, Prob& P
             }
             D[WBC_DBG_M + e] = v;
         }
-        if (lane < 18) {
+        for (int ln = lane; ln < 18; ln += SUB) {
             // register selects (a pointer select into hb[] would put hb in scratch memory)
             double v6 = hb[0];
 #pragma unroll
-            for (int k = 1; k < 6; ++k) v6 = (lane == k) ? hb[k] : v6;
-            D[WBC_DBG_CNU + lane] = (lane < 6) ? v6 : s.hj[lane - 6];
+            for (int k = 1; k < 6; ++k) v6 = (ln == k) ? hb[k] : v6;
+            D[WBC_DBG_CNU + ln] = (ln < 6) ? v6 : s.hj[ln - 6];
         }
-        for (int e = lane; e < 216; e += 64) {
+        for (int e = lane; e < 216; e += SUB) {
             const int i = e / 18, j = e % 18, l = i / 3, rr = i % 3;
             double v, vb;
             if (j < 3) {
@@ -874,14 +970,14 @@ __device__ void update_phase(const KernelArgs& a, int rb, UpdScratch& s, Prob& P
             D[WBC_DBG_RSW + lane] = P.rsw[lane];
             D[WBC_DBG_BBAR + 6 + lane] = P.bbj[lane];
         }
-        if (lane < 36) {
-            const int i = lane / 6, j = lane % 6;
+        for (int ln = lane; ln < 36; ln += SUB) {
+            const int i = ln / 6, j = ln % 6;
             double v = 0.0;
             if (i < 3 && j < 3) v = (i == j) ? m : 0.0;
             else if (i >= 3 && j >= 3) v = P.Ic[3 * (i - 3) + (j - 3)];
-            D[WBC_DBG_MBARB + lane] = v;
+            D[WBC_DBG_MBARB + ln] = v;
         }
-        for (int e = lane; e < 144; e += 64) D[WBC_DBG_MBARJ + e] = P.Mbj[e];
+        for (int e = lane; e < 144; e += SUB) D[WBC_DBG_MBARJ + e] = P.Mbj[e];
     }
     wsync();
 }
@@ -1004,7 +1100,7 @@ __device__ __forceinline__ void to_column(QpScratch& s, double* cc) {
 // d = C[:, p] broadcast from lane p (uniform, v_readlane)
 __device__ __forceinline__ void read_column(const double* cc, int p, double* d) {
 #pragma unroll
-    for (int k = 0; k < NQ; ++k) d[k] = bcast(cc[k], p);
+    for (int k = 0; k < NQ; ++k) d[k] = WBC_LOOP_BPERM ? vbcast(cc[k], p) : bcast(cc[k], p);
 }
 __device__ __forceinline__ void zero_rinv(QpScratch& s) {
     double2* r = &s.Rv[0][0];
@@ -1271,7 +1367,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
                 lds_sync();
 #else
 #pragma unroll
-                for (int k = 0; k < NQ; ++k) d[k] = (k >= e) ? bcast(cc[k], e) : 0.0;
+                for (int k = 0; k < NQ; ++k) d[k] = (k >= e) ? (WBC_EQ_BPERM ? vbcast(cc[k], e) : bcast(cc[k], e)) : 0.0;
 #endif
                 const bool add = !(zn <= tiny * fmax(1.0, bcast(nn, e)));
                 // Householder reflection on rows e..23 (static q = e)
@@ -1641,17 +1737,29 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
 // ---------------------------------------------------------------------------------------
 #define WBC_KERNEL_ATTR \
     __global__ __attribute__((amdgpu_flat_work_group_size(64, 64), amdgpu_waves_per_eu(WBC_WAVES_PER_SIMD)))
-// Update-kernel occupancy: 2, 3 and 4 waves per SIMD time the same (the phase is VALU-bound,
-// profiles/r01/split_probe.log); 2 keeps it spill-free
+// Split-mode update kernel: WBC_UPDATE_SUB lanes per robot, 64 / SUB robots per wave.  16 (four
+// robots per wave) is the default: the update phase keeps at most 13 lanes of a robot busy, so a
+// 64-lane robot wastes 3/4 of every VALU issue.  Four robots' scratch (36 KB of LDS per
+// workgroup) limits the kernel to one wave per SIMD; measured on MI355X it still beats the
+// one-robot-per-wave update (which runs at 2 waves per SIMD) and the fused kernel: B = 4096
+// stance 110.0 -> 100.3 us per step, B = 16384 342 -> 310 us (profiles/r01/variants_update_sub.log).
+#ifndef WBC_UPDATE_SUB
+#define WBC_UPDATE_SUB 16
+#endif
 #ifndef WBC_UPDATE_WAVES_PER_SIMD
-#define WBC_UPDATE_WAVES_PER_SIMD 2
+#define WBC_UPDATE_WAVES_PER_SIMD (WBC_UPDATE_SUB == 16 ? 1 : 2)
 #endif
 #define WBC_UPDATE_KERNEL_ATTR \
     __global__ __attribute__((amdgpu_flat_work_group_size(64, 64), amdgpu_waves_per_eu(WBC_UPDATE_WAVES_PER_SIMD)))
-
+// wbc_step's default form: 1 = update kernel + solve kernel (the problem passes through HBM,
+// 2.9 KB per robot each way), 0 = the fused kernel
+#ifndef WBC_DEFAULT_SPLIT
+#define WBC_DEFAULT_SPLIT 1
+#endif
+constexpr int UPD_SUB = WBC_UPDATE_SUB, UPD_RPW = 64 / UPD_SUB;
 struct UpdLds {
-    Prob prob;
-    UpdScratch u;
+    Prob prob[UPD_RPW];
+    UpdScratch u[UPD_RPW];
 };
 struct SolveLds {
     Prob prob;
@@ -1663,7 +1771,7 @@ WBC_KERNEL_ATTR void wbc_step_kernel(KernelArgs a) {
     const int rb = xcd_robot();
     if (rb >= a.batch) return;
     STAMP(a, rb, 0);
-    update_phase(a, rb, L.u, L.prob);
+    update_phase<64>(a, rb, lane_id(), true, L.u, L.prob);
     STAMP(a, rb, 1);
     solve_phase(a, rb, L.prob, L.q);
     STAMP(a, rb, 6);
@@ -1671,12 +1779,21 @@ WBC_KERNEL_ATTR void wbc_step_kernel(KernelArgs a) {
 
 WBC_UPDATE_KERNEL_ATTR void wbc_update_kernel(KernelArgs a) {
     __shared__ UpdLds L;
-    const int rb = xcd_robot();
-    if (rb >= a.batch) return;
-    update_phase(a, rb, L.u, L.prob);
-    const double2* src = reinterpret_cast<const double2*>(&L.prob);
+    int seg, lane, rb;
+    if constexpr (UPD_SUB == 64) {
+        seg = 0; lane = lane_id(); rb = xcd_robot();
+        if (rb >= a.batch) return;
+    } else {
+        seg = (int)threadIdx.x / UPD_SUB; lane = (int)threadIdx.x % UPD_SUB;
+        rb = (int)blockIdx.x * UPD_RPW + seg;
+    }
+    const bool wr = rb < a.batch;  // a padding segment recomputes the last robot, writes nothing
+    if (!wr) rb = a.batch - 1;
+    update_phase<UPD_SUB>(a, rb, lane, wr, L.u[seg], L.prob[seg]);
+    const double2* src = reinterpret_cast<const double2*>(&L.prob[seg]);
     double2* dst = reinterpret_cast<double2*>(a.work + (size_t)rb * PROB_LEN);
-    for (int k = lane_id(); k < PROB_LEN / 2; k += 64) dst[k] = src[k];
+    if (wr)
+        for (int k = lane; k < PROB_LEN / 2; k += UPD_SUB) dst[k] = src[k];
 }
 
 WBC_KERNEL_ATTR void wbc_solve_kernel(KernelArgs a) {
@@ -1705,8 +1822,9 @@ extern "C" hipError_t wbc_launch_step(const wbc::KernelArgs* a, hipStream_t st) 
     hipLaunchKernelGGL(wbc::wbc_step_kernel, dim3(a->batch), dim3(64), 0, st, *a);
     return hipGetLastError();
 }
+extern "C" int wbc_kernel_default_split() { return WBC_DEFAULT_SPLIT; }
 extern "C" hipError_t wbc_launch_update(const wbc::KernelArgs* a, hipStream_t st) {
-    hipLaunchKernelGGL(wbc::wbc_update_kernel, dim3(a->batch), dim3(64), 0, st, *a);
+    hipLaunchKernelGGL(wbc::wbc_update_kernel, dim3((a->batch + wbc::UPD_RPW - 1) / wbc::UPD_RPW), dim3(64), 0, st, *a);
     return hipGetLastError();
 }
 extern "C" hipError_t wbc_launch_solve(const wbc::KernelArgs* a, hipStream_t st) {

@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 import wbc_np as W
-from quadrupedwholebodycontroller_amd import DEBUG, SPLIT, STATELESS, Engine, split_debug, workloads
+from quadrupedwholebodycontroller_amd import DEBUG, FUSED, SPLIT, STATELESS, Engine, split_debug, workloads
 
 pytestmark = pytest.mark.gpu
 
@@ -86,7 +86,7 @@ def test_update_solve_split_equals_fused():
     e = Engine(B)
     e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
     e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
-    e.step(STATELESS)  # one fused kernel (default)
+    e.step(STATELESS | FUSED)  # one fused kernel
     fused = e.outputs()
     e.update(STATELESS)
     e.solve(STATELESS)

@@ -3,7 +3,7 @@ Usage (GPU box): WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_istamps.so 
 import json, os, sys
 import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from quadrupedwholebodycontroller_amd import STATELESS, Engine, workloads
+from quadrupedwholebodycontroller_amd import FUSED, STATELESS, Engine, workloads
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "stance_cold"
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
@@ -12,7 +12,7 @@ e = Engine(B)
 e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
 e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
 for _ in range(3):
-    e.step(STATELESS)  # the stamps live in the fused kernel
+    e.step(STATELESS | FUSED)  # the stamps live in the fused kernel
 e.synchronize()
 d = e.debug()[:, 0:6]
 out = e.outputs()

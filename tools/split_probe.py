@@ -6,7 +6,7 @@ CHILD = r'''
 import json, sys
 sys.path.insert(0, %r)
 import numpy as np, torch
-from quadrupedwholebodycontroller_amd import NO_X, STATELESS, Engine, workloads
+from quadrupedwholebodycontroller_amd import FUSED, NO_X, STATELESS, Engine, workloads
 steps = int(sys.argv[1]); F = STATELESS | NO_X
 res = {}
 for name, gen, B in (("stance_cold_b4096", workloads.stance_cold, 4096), ("rl_random_b8192", workloads.rl_random, 8192)):
@@ -19,7 +19,7 @@ for name, gen, B in (("stance_cold_b4096", workloads.stance_cold, 4096), ("rl_ra
         a.record(st)
         for _ in range(steps): fn()
         b.record(st); torch.cuda.synchronize(); return a.elapsed_time(b) / steps
-    fused = t(lambda: e.step(F)); o1 = e.outputs()
+    fused = t(lambda: e.step(F | FUSED)); o1 = e.outputs()
     upd = t(lambda: e.update(F))
     split = t(lambda: (e.update(F), e.solve(F))); o2 = e.outputs()
     res[name] = dict(fused_ms=fused, update_ms=upd, split_ms=split, same=bool(np.array_equal(o1["tau"], o2["tau"])))

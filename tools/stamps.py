@@ -3,7 +3,7 @@ Usage (GPU box): WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_stamps.so p
 import json, os, sys
 import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from quadrupedwholebodycontroller_amd import STATELESS, Engine, workloads
+from quadrupedwholebodycontroller_amd import FUSED, STATELESS, Engine, workloads
 from quadrupedwholebodycontroller_amd._capi import DBG
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "stance_cold"
@@ -13,7 +13,7 @@ e = Engine(B)
 e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
 e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
 for _ in range(3):
-    e.step(STATELESS)  # the stamps live in the fused kernel
+    e.step(STATELESS | FUSED)  # the stamps live in the fused kernel
 e.synchronize()
 d = e.debug()[:, DBG["STAMPS"]:DBG["STAMPS"] + 7]
 names = ["update", "qp_setup(H_s chol, x0)", "normals+C0", "GI loop", "primal recovery", "outputs"]
