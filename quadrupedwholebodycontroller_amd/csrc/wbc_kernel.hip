@@ -240,7 +240,7 @@ __device__ __forceinline__ bool seg_any(bool p) {
 #define WBC_EQ_BPERM 0
 #endif
 #ifndef WBC_LOOP_BPERM
-#define WBC_LOOP_BPERM 0
+#define WBC_LOOP_BPERM 1  // measured: B = 4096 stance 100.5 -> 95.4 us, rl_random B = 8192 453 -> 376 us (profiles/r01/variants_loop_bperm.log)
 #endif
 #ifndef WBC_XCD_REMAP
 #define WBC_XCD_REMAP 0
@@ -1142,14 +1142,37 @@ __device__ __forceinline__ double householder(int q, bool add, double zn, double
     for (int k = 0; k < NQ; ++k) cc[k] -= vw * v[k];
     return ia;
 }
-__device__ __forceinline__ void add_column(QpScratch& s, int q, bool add, double zn, double dq, double rk,
-                                           double* v, double* cc) {
+__device__ __forceinline__ void store_rinv_column(QpScratch& s, int q, bool add, double ia, double rk) {
     const int lane = lane_id();
-    const double ia = householder(q, add, zn, dq, v, cc);
     if (add && lane <= q) {
         double* col = reinterpret_cast<double*>(&s.Rv[q >> 1][lane]) + (q & 1);
         *col = (lane == q) ? ia : -rk * ia;
     }
+}
+__device__ __forceinline__ void add_column(QpScratch& s, int q, bool add, double zn, double dq, double rk,
+                                           double* v, double* cc) {
+    store_rinv_column(s, q, add, householder(q, add, zn, dq, v, cc), rk);
+}
+// The same reflection without forming v: v = d2 - alpha e_q, so v^T c = cz - alpha c[q] and
+// c -= vw v is c -= vw d2 plus vw alpha at row q.  d2 (the column masked to rows >= q), cz = c^T d2
+// and cq = c[q] come in precomputed with fp64 0 / 1 row masks (one multiply or FMA per row instead
+// of a two-instruction v_cndmask select per row for every dynamic-position insert and extract).
+__device__ __forceinline__ double householder_masked(int q, bool add, double zn, double dq, double cz, double cq,
+                                                     const double* d2, double* cc) {
+    if (!add) { zn = 1.0; dq = 0.0; }
+    const double rs = fast_rsq(zn);
+    const double nrm2 = zn * rs;
+    const double alpha = (dq >= 0.0) ? -nrm2 : nrm2;
+    const double ia = (dq >= 0.0) ? -rs : rs;
+    const double beta = fast_rcp(zn + nrm2 * fabs(dq));
+    const double vw = add ? (cz - alpha * cq) * beta : 0.0;
+    const double vwa = vw * alpha;
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+        const double ok = (k == q) ? 1.0 : 0.0;
+        cc[k] = fma(vwa, ok, fma(-vw, d2[k], cc[k]));
+    }
+    return ia;
 }
 
 // Multipliers and slacks of the point where every active constraint (slots 0..q-1, constraint
@@ -1558,17 +1581,19 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
         read_column(cc, col, d);
         IST(1);  // column broadcast
         const double rk = rinv_times_d(s, d);
-        double dq = 0.0;
+        // d2 = rows >= pos of d, cq = this lane's c[pos] (fp64 0 / 1 row masks, uniform)
+        double czp[4] = {0.0, 0.0, 0.0, 0.0}, cqp[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int k = 0; k < NQ; ++k) {
-            dq = (k == pos) ? d[k] : dq;
-            d[k] = (k >= pos) ? d[k] : 0.0;  // d2 (rows >= pos)
+            const double mk = (k >= pos) ? 1.0 : 0.0, ok = (k == pos) ? 1.0 : 0.0;
+            d[k] *= mk;
+            czp[k & 3] += cc[k] * d[k];
+            cqp[k & 3] += cc[k] * ok;
         }
-        double czp[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int k = 0; k < NQ; ++k) czp[k & 3] += cc[k] * d[k];
         const double cz = (czp[0] + czp[1]) + (czp[2] + czp[3]);  // (C2^T d2)_p = n_p^T z
+        const double cq = (cqp[0] + cqp[1]) + (cqp[2] + cqp[3]);  // exact: one non-zero term
         const double zn = bcast(cz, col);                   // |d2|^2: lane col holds d itself
+        const double dq = bcast(cq, col);                   // d[pos]
         IST(2);  // R^-1 d, n^T z, |z|^2
 
         // step (skipped in rebuild mode: the active set is re-added as is)
@@ -1614,7 +1639,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
         }
         IST(3);  // step length, multipliers
         // one in-place update site for every path (no second live copy of cc)
-        add_column(s, pos, add, zn, dq, rk, d, cc);
+        store_rinv_column(s, pos, add, householder_masked(pos, add, zn, dq, cz, cq, d, cc), rk);
         IST(4);  // Householder update
         if (add) {
             if (rebuild) {
