@@ -25,14 +25,16 @@ HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 # algorithmic flops per solve F(k) = F_dyn + F_asm + F_tau + F_fact + k F_iter
 F_DYN, F_ASM, F_TAU, F_FACT, F_ITER = 9000, 14000, 600, 24696, 12936
 BYTES_COLD = 929          # 729 B in + 200 B out per cold solve
+BYTES_IN, BYTES_OUT = 729, 200  # per state read / per QP written (mode hypotheses share the state read)
 
 CONFIGS = {
     "stance_cold_b4096": dict(gen="stance_cold", batch=4096, seed=1,
                               desc="BASELINE configs[1]: B=4096 4-contact stance QPs, fp64, cold start"),
     "rl_random_b8192": dict(gen="rl_random", batch=8192, seed=3,
                             desc="BASELINE configs[3] per-GPU shard: randomized q/qd, 16 contact masks, cold"),
-    "modes16_b16384": dict(gen="modes16", batch=16384, seed=4,
-                           desc="BASELINE configs[4] per-GPU shard: 1024 states x all 16 contact masks, cold"),
+    "modes16_b16384": dict(gen="modes16", batch=16384, seed=4, modes=16,
+                           desc="BASELINE configs[4] per-GPU shard: 1024 states x all 16 contact masks, cold; "
+                                "wbc_step_modes (dynamics + assembly once per state, 16 QPs per state)"),
 }
 
 
@@ -99,6 +101,24 @@ def committed_traffic(workload, batch):
                 rec.get("batch") == batch and "traffic" in rec):
             return rec["traffic"], os.path.relpath(f, ROOT)
     return {}, None
+
+
+def make_engine(cfg, B, seed, device, stream):
+    """Engine for a bench config on `stream`, inputs loaded; returns (engine, step flags fn, inputs).
+    Mode-hypothesis configs hold B / K states and step with wbc_step_modes."""
+    from quadrupedwholebodycontroller_amd import Engine, workloads
+
+    K = cfg.get("modes", 0)
+    e = Engine(B, device=device)
+    e.set_stream(stream.cuda_stream)
+    if K:
+        inp, modes = workloads.mode_states(B // K, seed)
+        e.set_modes(modes)
+    else:
+        inp = getattr(workloads, cfg["gen"])(B, seed=seed)
+    e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
+    e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
+    return e, (e.step_modes if K else e.step), inp
 
 
 def bench_trot(torch, stream, device, STATELESS, B=4096, T=400, seed=2):
@@ -172,23 +192,20 @@ def main():
 
     cfg = CONFIGS[args.config]
     B = args.batch or cfg["batch"]
-    gen = getattr(workloads, cfg["gen"])
-    inp = gen(B, seed=cfg["seed"] + 1000 * rank)
+    K = cfg.get("modes", 0)
+    S = B // K if K else B  # input rows (states)
 
     # a dedicated (non-null) stream: the engine launches on it, the RCCL all-gather is ordered on it,
     # and the HIP events below time it (the legacy null stream would be handle 0 = "engine default")
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
-    e = Engine(B, device=local_rank)
-    e.set_stream(stream.cuda_stream)
-    e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
-    e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
+    e, step, inp = make_engine(cfg, B, cfg["seed"] + 1000 * rank, local_rank, stream)
     tau_local = torch.zeros(B * 12, dtype=torch.float64, device="cuda")
     e.bind_device_outputs(tau=tau_local.data_ptr())
     tau_all = torch.zeros(world * B * 12, dtype=torch.float64, device="cuda") if world > 1 else None
 
     def one_step():
-        e.step(STEP_FLAGS)
+        step(STEP_FLAGS)
         if world > 1:
             dist.all_gather_into_tensor(tau_all, tau_local)
 
@@ -226,24 +243,35 @@ def main():
     # A step is two kernels (wbc_step's default form): the update kernel (dynamics + assembly, four
     # robots per wave) then the solve kernel (QP + torques).  Each is timed alone on the launch
     # stream; the dominant one (the solve kernel) carries the roofline.
-    step_ms = timed(lambda: e.step(STEP_FLAGS))
+    step_ms = timed(lambda: step(STEP_FLAGS))
     out = e.outputs()
     iters = out["iters"].astype(np.int64)
     status = out["status"]
-    upd_ms = timed(lambda: e.update(STEP_FLAGS))
-    solve_ms = timed(lambda: e.solve(STEP_FLAGS))  # re-solves the assembled problem (stateless)
+    if K:  # wbc_step_modes launches the pair together: the update of the S states is timed on an
+        # S-robot engine holding the same inputs, the solve kernel is the rest of the step
+        e_k = Engine(S, device=local_rank)
+        e_k.set_stream(stream.cuda_stream)
+        e_k.set_state(inp["base_pose"], inp["nu"], inp["qj"])
+        e_k.set_reference(inp["ref"], inp["contacts"], inp["switching"])
+        upd_ms = timed(lambda: e_k.update(STEP_FLAGS))
+        solve_ms = step_ms - upd_ms
+        e_k.close()
+    else:
+        upd_ms = timed(lambda: e.update(STEP_FLAGS))
+        solve_ms = timed(lambda: e.solve(STEP_FLAGS))  # re-solves the assembled problem (stateless)
     kernels = {"wbc_update_kernel": upd_ms, "wbc_solve_kernel": solve_ms}
     dom = max(kernels, key=kernels.get)
     dom_ms = kernels[dom]
     # flops owned by each kernel: dynamics + assembly in the update, factorisation + active-set
     # iterations + torques in the solve
-    flops_k = {"wbc_update_kernel": float(B * (F_DYN + F_ASM)),
+    flops_k = {"wbc_update_kernel": float(S * (F_DYN + F_ASM)),
                "wbc_solve_kernel": float(np.sum(F_TAU + F_FACT + F_ITER * iters))}
     tf_dom = flops_k[dom] / (dom_ms * 1e-3) / 1e12
-    hbm_gbs = B * BYTES_COLD / (step_ms * 1e-3) / 1e9
+    bytes_step = S * BYTES_IN + B * BYTES_OUT
+    hbm_gbs = bytes_step / (step_ms * 1e-3) / 1e9
 
     breakdown = None
-    if args.breakdown:  # the fused single-kernel form of the same step, for comparison
+    if args.breakdown and not K:  # the fused single-kernel form of the same step, for comparison
         breakdown = dict(fused_step_ms=timed(lambda: e.step(STEP_FLAGS | FUSED)), split_step_ms=step_ms)
 
     extra = {}
@@ -253,14 +281,10 @@ def main():
             if name == args.config:
                 continue
             B2 = c2["batch"]
-            inp2 = getattr(workloads, c2["gen"])(B2, seed=c2["seed"])
-            e2 = Engine(B2, device=local_rank)
-            e2.set_stream(stream.cuda_stream)
-            e2.set_state(inp2["base_pose"], inp2["nu"], inp2["qj"])
-            e2.set_reference(inp2["ref"], inp2["contacts"], inp2["switching"])
+            e2, step2, _ = make_engine(c2, B2, c2["seed"], local_rank, stream)
             for _ in range(args.warmup):
-                e2.step(STEP_FLAGS)
-            ms2 = timed(lambda: e2.step(STEP_FLAGS))
+                step2(STEP_FLAGS)
+            ms2 = timed(lambda: step2(STEP_FLAGS))
             o2 = e2.outputs()
             extra[name] = dict(batch=B2, ms_per_step=ms2, solves_per_s=B2 / (ms2 * 1e-3),
                                status_counts=np.bincount(o2["status"], minlength=4).tolist(),
@@ -294,11 +318,12 @@ def main():
                              "flops of SURVEY 8(d) owned by this kernel (F_fact + F_tau + k F_iter, k = iters[] per "
                              "robot); latency/issue-bound small dense linear algebra"},
         "roofline_hbm": {"bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": hbm_gbs / HBM_PEAK_GBS, "bytes_per_solve": BYTES_COLD,
+                         "frac": hbm_gbs / HBM_PEAK_GBS, "bytes_per_solve": bytes_step / B,
                          "traffic": (traffic.get("wbc_update_kernel", 0) + traffic.get("wbc_solve_kernel", 0))
                          if traffic else None,
-                         "note": "algorithmic 929 B/solve over the step (both kernels); traffic = PMC bytes per "
-                                 "step (both kernels, incl. the 2.9 KB/robot problem hand-off)"},
+                         "note": "algorithmic bytes over the step (both kernels): 729 B read per state + 200 B "
+                                 "written per QP (929 B/solve one QP per state); traffic = PMC bytes per step "
+                                 "(both kernels, incl. the 2.9 KB/state problem hand-off)"},
         "qp_status_counts": np.bincount(status, minlength=4).tolist(),
         "mean_iters": float(iters.mean()),
     }

@@ -184,6 +184,18 @@ int32_t wbc_solve(wbc_engine* h, uint32_t flags);
 int32_t wbc_step(wbc_engine* h, uint32_t flags);
 int32_t wbc_synchronize(wbc_engine* h);
 
+/* Contact-mode hypotheses (BASELINE configs[4]: every state solved under several contact masks).
+ * After wbc_set_modes(h, K, modes) with K dividing the batch B, the engine holds S = B / K states:
+ * wbc_set_state / wbc_set_reference / bound device inputs hold S rows (contacts[] is not read), and
+ * wbc_step_modes computes the dynamics and assembly (updateState, cpp:256-294) once per state, then
+ * solves K QPs per state: output row s * K + k is state s under contact mask modes[k] (4-bit,
+ * footContacts_ order), bit-identical to a wbc_step on that state with contacts = modes[k].
+ * Hypotheses are cold steps: flags must include WBC_STATELESS (WBC_DEBUG is refused).
+ * wbc_update / wbc_solve / wbc_step return WBC_ERR_STATE while modes are set; K = 0 clears them. */
+#define WBC_MAX_MODES 16
+int32_t wbc_set_modes(wbc_engine* h, int32_t n_modes, const uint8_t* modes);
+int32_t wbc_step_modes(wbc_engine* h, uint32_t flags);
+
 /* Outputs (host copies, synchronous).  Any pointer may be NULL.
  * tau [B][12], grf [B][12] (= x[18:30]), x [B][42], status [B], iters [B]. */
 int32_t wbc_get_output(wbc_engine* h, double* tau, double* grf, double* x, int32_t* status,

@@ -26,7 +26,7 @@ DBG = dict(COM=0, COMVEL=3, POSE=6, VC=12, M=18, CNU=342, JFEET=360, PFEET=576, 
 C_API_SYMBOLS = [
     "wbc_default_params", "wbc_anymal_model", "wbc_create", "wbc_destroy", "wbc_batch", "wbc_set_stream",
     "wbc_set_state", "wbc_set_reference", "wbc_bind_device_inputs", "wbc_bind_device_outputs", "wbc_reset", "wbc_update", "wbc_solve",
-    "wbc_step", "wbc_synchronize", "wbc_get_output", "wbc_device_outputs", "wbc_get_debug", "wbc_last_kernel_ms",
+    "wbc_step", "wbc_set_modes", "wbc_step_modes", "wbc_synchronize", "wbc_get_output", "wbc_device_outputs", "wbc_get_debug", "wbc_last_kernel_ms",
     "wbc_last_error", "wbc_model_from_urdf",
 ]
 
@@ -85,6 +85,8 @@ def load_library(path: str = LIB_PATH):
         "wbc_update": ([P, U32], I32),
         "wbc_solve": ([P, U32], I32),
         "wbc_step": ([P, U32], I32),
+        "wbc_set_modes": ([P, I32, P], I32),
+        "wbc_step_modes": ([P, U32], I32),
         "wbc_synchronize": ([P], I32),
         "wbc_get_output": ([P, P, P, P, P, P], I32),
         "wbc_device_outputs": ([P, C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(P)], I32),
@@ -146,6 +148,7 @@ class Engine:
     def __init__(self, batch: int, device: int = 0, params: WbcParams | None = None, model: WbcModel | None = None):
         self.lib = load_library()
         self.batch = int(batch)
+        self.n_modes = 0
         self.h = C.c_void_p()
         rc = self.lib.wbc_create(C.byref(model) if model else None, C.byref(params) if params else None,
                                  self.batch, int(device), C.byref(self.h))
@@ -167,14 +170,19 @@ class Engine:
             pass
 
     # --- inputs -------------------------------------------------------------------------
+    @property
+    def input_rows(self) -> int:
+        """Rows of the input arrays: B robots, or B / K states under K mode hypotheses."""
+        return self.batch // self.n_modes if self.n_modes else self.batch
+
     def set_state(self, base_pose=None, nu=None, qj=None):
-        B = self.batch
+        B = self.input_rows
         arrs = [None if v is None else np.ascontiguousarray(v, np.float64).reshape(B, n)
                 for v, n in ((base_pose, POSE_LEN), (nu, NU_LEN), (qj, NUM_JOINTS))]
         self._check(self.lib.wbc_set_state(self.h, *[_ptr(a) for a in arrs]), "wbc_set_state")
 
     def set_reference(self, ref=None, contacts=None, switching=None):
-        B = self.batch
+        B = self.input_rows
         r = None if ref is None else np.ascontiguousarray(ref, np.float64).reshape(B, REF_LEN)
         c = None if contacts is None else np.ascontiguousarray(contacts, np.uint8).reshape(B)
         s = None if switching is None else np.ascontiguousarray(switching, np.uint8).reshape(B)
@@ -207,6 +215,17 @@ class Engine:
 
     def step(self, flags: int = 0):
         self._check(self.lib.wbc_step(self.h, flags), "wbc_step")
+
+    def set_modes(self, modes=None):
+        """wbc_set_modes: solve every state under each contact mask in `modes` (None / [] clears)."""
+        m = None if modes is None or len(modes) == 0 else np.ascontiguousarray(modes, np.uint8).ravel()
+        n = 0 if m is None else m.size
+        self._check(self.lib.wbc_set_modes(self.h, n, _ptr(m)), "wbc_set_modes")
+        self.n_modes = n
+
+    def step_modes(self, flags: int = 1):
+        """wbc_step_modes: one cold step of every (state, mode) hypothesis (flags need STATELESS)."""
+        self._check(self.lib.wbc_step_modes(self.h, flags), "wbc_step_modes")
 
     def synchronize(self):
         self._check(self.lib.wbc_synchronize(self.h), "wbc_synchronize")

@@ -48,6 +48,9 @@ struct wbc_engine {
     uint8_t* d_contacts = nullptr;
     uint8_t* d_switching = nullptr;
     uint8_t* d_mask = nullptr;
+    // contact-mode hypotheses (wbc_set_modes): n_modes > 0 turns the inputs into B / n_modes states
+    int32_t n_modes = 0;
+    uint8_t* d_modes = nullptr;
     // bound (possibly external) inputs
     const double* in_pose = nullptr;
     const double* in_nu = nullptr;
@@ -82,6 +85,9 @@ hipError_t dalloc(T** p, size_t n) {
     return hipMalloc(reinterpret_cast<void**>(p), sizeof(T) * (n ? n : 1));
 }
 
+// rows of the input arrays: one per robot, or one per state when mode hypotheses are set
+size_t input_rows(const wbc_engine* h) { return (size_t)(h->n_modes ? h->batch / h->n_modes : h->batch); }
+
 wbc::KernelArgs make_args(wbc_engine* h, uint32_t flags) {
     wbc::KernelArgs a;
     a.model = h->d_model;
@@ -104,6 +110,8 @@ wbc::KernelArgs make_args(wbc_engine* h, uint32_t flags) {
     a.stateful = (flags & WBC_STATELESS) ? 0 : 1;
     a.debug = (flags & WBC_DEBUG) ? 1 : 0;
     a.cold = (flags & WBC_COLD) ? 1 : 0;
+    a.modes = 0;
+    a.mode_masks = h->d_modes;
     return a;
 }
 }  // namespace
@@ -170,6 +178,7 @@ int32_t wbc_create(const wbc_model* model, const wbc_params* params, int32_t bat
     ALLOC(d_contacts, B);
     ALLOC(d_switching, B);
     ALLOC(d_mask, B);
+    ALLOC(d_modes, WBC_MAX_MODES);
     ALLOC(d_hist, B * wbc::HIST_LEN);
     ALLOC(d_work, B * wbc::PROB_LEN);
     ALLOC(d_tau, B * WBC_NUM_JOINTS);
@@ -224,7 +233,7 @@ int32_t wbc_destroy(wbc_engine* h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     void* ptrs[] = {h->d_model, h->d_params, h->d_pose, h->d_nu, h->d_qj, h->d_ref, h->d_contacts, h->d_switching,
-                    h->d_mask, h->d_hist, h->d_work, h->d_tau, h->d_grf, h->d_x, h->d_status, h->d_iters, h->d_dbg};
+                    h->d_mask, h->d_modes, h->d_hist, h->d_work, h->d_tau, h->d_grf, h->d_x, h->d_status, h->d_iters, h->d_dbg};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
@@ -245,7 +254,7 @@ int32_t wbc_set_stream(wbc_engine* h, void* stream) {
 int32_t wbc_set_state(wbc_engine* h, const double* base_pose, const double* nu, const double* qj) {
     if (!h) return fail(WBC_ERR_ARG, "null handle");
     WBC_HIP(hipSetDevice(h->device));
-    const size_t B = (size_t)h->batch;
+    const size_t B = input_rows(h);
     if (base_pose) { WBC_HIP(hipMemcpyAsync(h->d_pose, base_pose, B * WBC_POSE_LEN * sizeof(double), hipMemcpyHostToDevice, h->stream)); h->in_pose = h->d_pose; }
     if (nu) { WBC_HIP(hipMemcpyAsync(h->d_nu, nu, B * WBC_NU_LEN * sizeof(double), hipMemcpyHostToDevice, h->stream)); h->in_nu = h->d_nu; }
     if (qj) { WBC_HIP(hipMemcpyAsync(h->d_qj, qj, B * WBC_NUM_JOINTS * sizeof(double), hipMemcpyHostToDevice, h->stream)); h->in_qj = h->d_qj; }
@@ -256,7 +265,7 @@ int32_t wbc_set_state(wbc_engine* h, const double* base_pose, const double* nu, 
 int32_t wbc_set_reference(wbc_engine* h, const double* ref, const uint8_t* contacts, const uint8_t* switching) {
     if (!h) return fail(WBC_ERR_ARG, "null handle");
     WBC_HIP(hipSetDevice(h->device));
-    const size_t B = (size_t)h->batch;
+    const size_t B = input_rows(h);
     if (ref) { WBC_HIP(hipMemcpyAsync(h->d_ref, ref, B * WBC_REF_LEN * sizeof(double), hipMemcpyHostToDevice, h->stream)); h->in_ref = h->d_ref; }
     if (contacts) { WBC_HIP(hipMemcpyAsync(h->d_contacts, contacts, B, hipMemcpyHostToDevice, h->stream)); h->in_contacts = h->d_contacts; }
     if (switching) { WBC_HIP(hipMemcpyAsync(h->d_switching, switching, B, hipMemcpyHostToDevice, h->stream)); h->in_switching = h->d_switching; }
@@ -303,6 +312,7 @@ int32_t wbc_reset(wbc_engine* h, const uint8_t* mask) {
 
 int32_t wbc_update(wbc_engine* h, uint32_t flags) {
     if (!h) return fail(WBC_ERR_ARG, "null handle");
+    if (h->n_modes) return fail(WBC_ERR_STATE, "wbc_update: mode hypotheses are set (use wbc_step_modes, or wbc_set_modes(h, 0, NULL))");
     WBC_HIP(hipSetDevice(h->device));
     wbc::KernelArgs a = make_args(h, flags);
     WBC_HIP(wbc_launch_update(&a, h->stream));
@@ -312,6 +322,7 @@ int32_t wbc_update(wbc_engine* h, uint32_t flags) {
 
 int32_t wbc_solve(wbc_engine* h, uint32_t flags) {
     if (!h) return fail(WBC_ERR_ARG, "null handle");
+    if (h->n_modes) return fail(WBC_ERR_STATE, "wbc_solve: mode hypotheses are set (use wbc_step_modes, or wbc_set_modes(h, 0, NULL))");
     if (!h->updated) return fail(WBC_ERR_STATE, "wbc_solve before wbc_update");
     WBC_HIP(hipSetDevice(h->device));
     wbc::KernelArgs a = make_args(h, flags);
@@ -321,6 +332,7 @@ int32_t wbc_solve(wbc_engine* h, uint32_t flags) {
 
 int32_t wbc_step(wbc_engine* h, uint32_t flags) {
     if (!h) return fail(WBC_ERR_ARG, "null handle");
+    if (h->n_modes) return fail(WBC_ERR_STATE, "wbc_step: mode hypotheses are set (use wbc_step_modes, or wbc_set_modes(h, 0, NULL))");
     WBC_HIP(hipSetDevice(h->device));
     wbc::KernelArgs a = make_args(h, flags);
     const bool timed = (flags & WBC_TIMED) != 0;  // event packets cost a few us between kernels
@@ -333,6 +345,45 @@ int32_t wbc_step(wbc_engine* h, uint32_t flags) {
     } else {
         WBC_HIP(wbc_launch_step(&a, h->stream));
     }
+    if (timed) {
+        WBC_HIP(hipEventRecord(h->ev1, h->stream));
+        h->timed = true;
+    }
+    h->updated = false;
+    return WBC_OK;
+}
+
+int32_t wbc_set_modes(wbc_engine* h, int32_t n_modes, const uint8_t* modes) {
+    if (!h) return fail(WBC_ERR_ARG, "null handle");
+    if (n_modes == 0) {
+        h->n_modes = 0;
+        return WBC_OK;
+    }
+    if (n_modes < 0 || n_modes > WBC_MAX_MODES || !modes || h->batch % n_modes != 0)
+        return fail(WBC_ERR_ARG, "wbc_set_modes: need 1 <= n_modes <= WBC_MAX_MODES dividing the batch, and masks");
+    for (int32_t k = 0; k < n_modes; ++k)
+        if (modes[k] > 15) return fail(WBC_ERR_ARG, "wbc_set_modes: contact masks are 4-bit");
+    WBC_HIP(hipSetDevice(h->device));
+    WBC_HIP(hipMemcpyAsync(h->d_modes, modes, (size_t)n_modes, hipMemcpyHostToDevice, h->stream));
+    WBC_HIP(hipStreamSynchronize(h->stream));
+    h->n_modes = n_modes;
+    return WBC_OK;
+}
+
+int32_t wbc_step_modes(wbc_engine* h, uint32_t flags) {
+    if (!h) return fail(WBC_ERR_ARG, "null handle");
+    if (!h->n_modes) return fail(WBC_ERR_STATE, "wbc_step_modes: no mode hypotheses set (wbc_set_modes)");
+    if (!(flags & WBC_STATELESS)) return fail(WBC_ERR_ARG, "wbc_step_modes: hypotheses are cold steps (WBC_STATELESS)");
+    if (flags & WBC_DEBUG) return fail(WBC_ERR_ARG, "wbc_step_modes: no debug records for hypotheses");
+    WBC_HIP(hipSetDevice(h->device));
+    wbc::KernelArgs a = make_args(h, flags);
+    a.modes = h->n_modes;
+    const bool timed = (flags & WBC_TIMED) != 0;
+    if (timed) WBC_HIP(hipEventRecord(h->ev0, h->stream));
+    wbc::KernelArgs au = a;  // the update runs once per state
+    au.batch = h->batch / h->n_modes;
+    WBC_HIP(wbc_launch_update(&au, h->stream));
+    WBC_HIP(wbc_launch_solve(&a, h->stream));
     if (timed) {
         WBC_HIP(hipEventRecord(h->ev1, h->stream));
         h->timed = true;

@@ -858,14 +858,18 @@ __device__ void update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
 #pragma unroll
             for (int j = 0; j < 12; ++j) old += H[H_JBJOLD + i * 12 + j] * qd[j];
         }
+        // mode hypotheses (a.modes > 0, stateless): both bounds unmasked, the R1 bound as for a stance
+        // leg and the swing bound as for a swing leg; the solve kernel masks them per hypothesis
+        // (each is read only for legs of its own kind, so the masked values are bit-identical)
         const double kn = (kap >> l) & 1, ko = (kap_old >> l) & 1;
+        const double kr1 = a.modes ? 1.0 : kn, ksw = a.modes ? 0.0 : kn;
         double jc_dot = 0.0, js_dot = 0.0;
         if (!switching) {
-            jc_dot = (kn * cur - ko * old) / dt;
-            js_dot = ((1.0 - kn) * cur - (1.0 - ko) * old) / dt;
+            jc_dot = (kr1 * cur - ko * old) / dt;
+            js_dot = ((1.0 - ksw) * cur - (1.0 - ko) * old) / dt;
         }
         const double cmd = (ref[42 + i] + pr.kd_swing * (ref[30 + i] - s.vf[l][rr]) + pr.kp_swing * (ref[18 + i] - s.pf[l][rr])) *
-                           (1.0 - kn);
+                           (1.0 - ksw);
         P.r1[i] = -jc_dot;
         P.rsw[i] = cmd - js_dot;
     }
@@ -1825,9 +1829,22 @@ WBC_KERNEL_ATTR void wbc_solve_kernel(KernelArgs a) {
     __shared__ SolveLds L;
     const int rb = xcd_robot();
     if (rb >= a.batch) return;
+    // mode hypotheses: QP rb is hypothesis rb % modes of state rb / modes (one assembled problem
+    // per state, read by all of its hypotheses)
+    const int row = a.modes ? rb / a.modes : rb;
     double2* dst = reinterpret_cast<double2*>(&L.prob);
-    const double2* src = reinterpret_cast<const double2*>(a.work + (size_t)rb * PROB_LEN);
+    const double2* src = reinterpret_cast<const double2*>(a.work + (size_t)row * PROB_LEN);
     for (int k = lane_id(); k < PROB_LEN / 2; k += 64) dst[k] = src[k];
+    if (a.modes) {  // this hypothesis' contact mask on the unmasked bounds (update_phase)
+        const int kap = a.mode_masks[rb - row * a.modes] & 15;
+        const int lane = lane_id();
+        wsync();
+        if (lane < 12) {
+            if ((kap >> (lane / 3)) & 1) L.prob.rsw[lane] = 0.0;
+            else L.prob.r1[lane] = 0.0;
+        }
+        if (lane == 0) L.prob.kappa = (double)kap;
+    }
     wsync();
     solve_phase(a, rb, L.prob, L.q);
 }

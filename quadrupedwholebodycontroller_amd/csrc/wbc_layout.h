@@ -68,6 +68,8 @@ struct KernelArgs {
     int32_t stateful;   // read / write history
     int32_t debug;      // write debug records
     int32_t cold;       // stateful, but no QP hotstart (WBC_COLD)
+    int32_t modes;      // contact-mode hypotheses per state (wbc_step_modes); 0 = one QP per input row
+    const uint8_t* mode_masks;  // [modes]: contact mask of hypothesis k
 };
 
 

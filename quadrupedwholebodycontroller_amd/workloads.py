@@ -68,6 +68,13 @@ def mode_hypotheses(n_states=8192, seed=4):
     return rep
 
 
+def mode_states(n_states=8192, seed=4):
+    """Config 5 for wbc_set_modes / wbc_step_modes: the n_states states of mode_hypotheses (one input
+    row each) and the 16 contact masks; QP s * 16 + k of the engine equals row s * 16 + k of
+    mode_hypotheses(n_states, seed)."""
+    return rl_random(n_states, seed), np.arange(16, dtype=np.uint8)
+
+
 def modes16(B=16384, seed=4):
     """Config 5 shard of B QPs: B // 16 states, each under all 16 contact masks."""
     return mode_hypotheses(B // 16, seed)

@@ -17,7 +17,7 @@ step() {
 for s in ${STEPS:-smoke pytest bench prof}; do
   case $s in
     smoke)  step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    pytest) step pytest 600 python -m pytest tests -m gpu -x -q ;;
+    pytest) step pytest 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     bench)  step bench 400 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 ${BENCH_ARGS:-} ;;
     stamps) step stamps 300 env WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_stamps.so python tools/stamps.py stance_cold 4096 ;;
     istamps) step istamps 300 env WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_istamps.so python tools/istamps.py stance_cold 4096 ;;
