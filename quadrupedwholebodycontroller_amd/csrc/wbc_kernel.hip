@@ -239,6 +239,12 @@ __device__ __forceinline__ bool seg_any(bool p) {
 #ifndef WBC_EQ_BPERM
 #define WBC_EQ_BPERM 0
 #endif
+// Drop in the active-set loop: 1 = Givens deletion (the remaining slots' R columns and every
+// constraint column rotated in place, R^-1 updated by the same rotations), 0 = restart from the
+// initial columns C0 and re-add the remaining active set
+#ifndef WBC_GIVENS_DROP
+#define WBC_GIVENS_DROP 1
+#endif
 #ifndef WBC_LOOP_BPERM
 #define WBC_LOOP_BPERM 1  // measured: B = 4096 stance 100.5 -> 95.4 us, rl_random B = 8192 453 -> 376 us (profiles/r01/variants_loop_bperm.log)
 #endif
@@ -351,7 +357,9 @@ __device__ __forceinline__ double sel3(const double* v, int k) { return k == 0 ?
 #ifdef WBC_ISTAMPS
 #define IST_DECL                                          \
     unsigned long long ist_prev_ = __builtin_amdgcn_s_memtime(); \
-    unsigned long long ist_acc_[6] = {0, 0, 0, 0, 0, 0}
+    unsigned long long ist_acc_[6] = {0, 0, 0, 0, 0, 0}; \
+    int ist_cnt_[2] = {0, 0}
+#define IST_COUNT(i) (++ist_cnt_[i])
 #define IST(i)                                                       \
     do {                                                             \
         __builtin_amdgcn_sched_barrier(0);                           \
@@ -364,6 +372,8 @@ __device__ __forceinline__ double sel3(const double* v, int k) { return k == 0 ?
     do {                                                                                          \
         if (lane_id() == 0)                                                                       \
             for (int i_ = 0; i_ < 6; ++i_) (a).dbg[(size_t)(rb) * WBC_DBG_LEN + i_] = (double)ist_acc_[i_]; \
+        if (lane_id() == 0)                                                                       \
+            for (int i_ = 0; i_ < 2; ++i_) (a).dbg[(size_t)(rb) * WBC_DBG_LEN + 6 + i_] = (double)ist_cnt_[i_]; \
     } while (0)
 // update-phase boundaries: absolute clock into debug slots 8.. (same build)
 #define UST(a, rb, i)                                                                              \
@@ -379,6 +389,7 @@ __device__ __forceinline__ double sel3(const double* v, int k) { return k == 0 ?
 #define EST(a, rb, i) do { } while (0)
 #define IST_DECL do { } while (0)
 #define IST(i) do { } while (0)
+#define IST_COUNT(i) do { } while (0)
 #define IST_FLUSH(a, rb) do { } while (0)
 #endif
 
@@ -1179,6 +1190,52 @@ __device__ __forceinline__ double householder_masked(int q, bool add, double zn,
     return ia;
 }
 
+// Delete active slot l (Goldfarb-Idnani constraint drop, after the active lists were shifted and q
+// decremented): slots l..q-1 now hold the old slots l+1..q, whose R columns (in the lanes act[k])
+// have one sub-diagonal entry each.  Givens rotations G_k on rows (k, k+1), k = l..q-1, restore the
+// triangle; they apply to every lane's column (J <- J G^T keeps C = J^T N consistent) and to the
+// columns of R^-1, and the new R^-1 is R^-1 G^T without row l and column q (rows of the old inverse
+// shift up by one).  Row and column loops are unrolled with wave-uniform guards, so every register
+// index is static.
+__device__ void givens_drop(QpScratch& s, int l, int q, int act, double* cc) {
+    const int lane = lane_id();
+    const int i = lane < NQ ? lane : 0;
+    double rr[NQ];  // row i of R^-1
+#pragma unroll
+    for (int jj = 0; jj < NQ / 2; ++jj) {
+        const double2 v = s.Rv[jj][i];
+        rr[2 * jj] = v.x;
+        rr[2 * jj + 1] = v.y;
+    }
+#pragma unroll
+    for (int k = 0; k < NQ - 1; ++k) {
+        if (k >= l && k < q) {
+            const int pl = bcast_i(act, k);
+            const double a0 = bcast(cc[k], pl), b0 = bcast(cc[k + 1], pl);
+            const double r2 = a0 * a0 + b0 * b0;
+            const double rh = (r2 > 0.0) ? fast_rsq(r2) : 0.0;
+            const double c = (r2 > 0.0) ? a0 * rh : 1.0, sn = b0 * rh;
+            const double x = cc[k], y = cc[k + 1];
+            cc[k] = fma(c, x, sn * y);
+            cc[k + 1] = fma(c, y, -sn * x);
+            const double ra = rr[k], rb2 = rr[k + 1];
+            rr[k] = fma(c, ra, sn * rb2);
+            rr[k + 1] = fma(c, rb2, -sn * ra);
+        }
+    }
+    // rows >= l take the next row; the triangle below the diagonal, row >= q and column >= q are 0
+    const int src = lane + ((lane >= l) ? 1 : 0);
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+        const double v = __shfl(rr[k], src & 63);
+        rr[k] = (lane < q && k >= lane && k < q) ? v : 0.0;
+    }
+    if (lane < NQ) {
+#pragma unroll
+        for (int jj = 0; jj < NQ / 2; ++jj) s.Rv[jj][lane] = make_double2(rr[2 * jj], rr[2 * jj + 1]);
+    }
+}
+
 // Multipliers and slacks of the point where every active constraint (slots 0..q-1, constraint
 // act of slot lane) holds with equality, from the slacks sp0 at the unconstrained optimum x0:
 // R^T v = -s_A (v_i = -column i of R^-1 . s_A), u = R^-1 v, s = sp0 + C[0:q]^T v.  This is the state
@@ -1581,6 +1638,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
             pos = q;
         }
         IST(0);  // selection
+        IST_COUNT(0);  // loop passes that reach the column broadcast (adds, drops, rebuild re-adds)
         double d[NQ];
         read_column(cc, col, d);
         IST(1);  // column broadcast
@@ -1602,6 +1660,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
 
         // step (skipped in rebuild mode: the active set is re-added as is)
         bool add = true, drop = false;
+        int drop_slot = -1;
         if (rebuild && warm_phase == 1 && !(zn > tiny * fmax(1.0, bcast(nn, col)))) {
             add = false;  // a warm constraint dependent on the others: reject the warm set
             warm_fail = true;
@@ -1627,8 +1686,10 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
                 if (lane < q) u -= t * rk;
                 up += t;
                 if (!full) {
+                    IST_COUNT(1);  // drops
                     add = false;
                     drop = true;
+                    drop_slot = l1;
                     // drop active slot l1: shift the active list
                     const int dropped = bcast_i(act, l1);
                     if (lane == dropped) active = false;
@@ -1656,7 +1717,10 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
             }
             lds_sync();
         }
-        if (drop) {
+        if (drop && WBC_GIVENS_DROP) {
+            givens_drop(s, drop_slot, q, act, cc);
+            lds_sync();
+        } else if (drop) {
             // C restarts from C0 and the remaining active set is re-added (rebuild mode).
             const int pl = lane < C0_LANES ? lane : 0;
 #pragma unroll

@@ -7,7 +7,7 @@ from quadrupedwholebodycontroller_amd import FUSED, STATELESS, Engine, workloads
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "stance_cold"
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
-inp = getattr(workloads, cfg)(B, seed=1)
+inp = getattr(workloads, cfg)(B, seed=1 if cfg == "stance_cold" else 3)
 e = Engine(B)
 e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
 e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
@@ -22,6 +22,9 @@ it = out["iters"].astype(float)
 res = {n: dict(median=float(np.median(d[:, i])), mean=float(d[:, i].mean())) for i, n in enumerate(names)}
 res["total"] = float(np.median(d.sum(1)))
 res["mean_iters"] = float(it.mean())
+cnt = e.debug()[:, 6:8]
+res["mean_loop_passes"] = float(cnt[:, 0].mean())  # adds + drops + rebuild re-adds
+res["mean_drops"] = float(cnt[:, 1].mean())
 print(json.dumps(dict(config=cfg, batch=B, loop_cycles=res), indent=1))
 u = e.debug()[:, 8:19]
 un = ["inputs+sincos", "stage A (leg chains)", "stage B (bodies)", "Jf + CoM sums", "Ic sum+inv", "stage C (joints)",

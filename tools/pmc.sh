@@ -16,4 +16,4 @@ for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU S
   echo "pass$i [$set] rc=$rc" >> $OUT/passes.txt
   if [ $rc -ne 0 ]; then echo "pmc pass $i failed rc=$rc"; tail -5 $OUT/pass$i.log; if [ $rc -ne 1 ]; then exit $rc; fi; fi
 done
-python3 tools/pmc_summary.py $OUT $OUT/pmc_summary.json stance_cold_b4096 4096 > /dev/null
+python3 tools/pmc_summary.py $OUT $OUT/pmc_summary.json stance_cold_b4096 4096 wbc_update_kernel,wbc_solve_kernel > /dev/null

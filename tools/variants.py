@@ -26,6 +26,22 @@ for name, gen, B in (("stance_cold_b4096", workloads.stance_cold, 4096), ("rl_ra
     res[name] = dict(ms=ms, solves_per_s=B / ms * 1e3, status=[int(x) for x in __import__("numpy").bincount(o["status"], minlength=4)],
                      tau_sum=float(abs(o["tau"]).sum()))
     e.close()
+S = 1024  # configs[4] shard: 1024 states x 16 contact masks through wbc_step_modes
+inp, modes = workloads.mode_states(S, 4)
+e = Engine(S * 16)
+st = torch.cuda.Stream(); torch.cuda.set_stream(st); e.set_stream(st.cuda_stream)
+e.set_modes(modes)
+e.set_state(inp["base_pose"], inp["nu"], inp["qj"]); e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
+for _ in range(3): e.step_modes(STATELESS | NO_X)
+ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+ev0.record(st)
+for _ in range(steps): e.step_modes(STATELESS | NO_X)
+ev1.record(st); torch.cuda.synchronize()
+ms = ev0.elapsed_time(ev1) / steps
+o = e.outputs()
+res["modes16_b16384"] = dict(ms=ms, solves_per_s=S * 16 / ms * 1e3, status=[int(x) for x in __import__("numpy").bincount(o["status"], minlength=4)],
+                             tau_sum=float(abs(o["tau"]).sum()))
+e.close()
 print(json.dumps(res))
 ''' % ROOT
 steps = sys.argv[1] if len(sys.argv) > 1 else "30"
