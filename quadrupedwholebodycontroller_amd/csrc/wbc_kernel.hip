@@ -70,6 +70,7 @@ struct QpScratch {
     double xs[12];          // slot part of x0 = -H^-1 g
     double ild[12];         // 1 / L_kk
     union {
+        double G[12][12];   // setup -> constraint normals: slot coupling Jc_com Mbar_b^-1 Jc_com^T
         double Rm[12][12];  // equality block: Rm[i][k] = R[k][i]
         double ucon[64];    // after the active-set loop: the primal y (24)
     };
@@ -1037,8 +1038,8 @@ __device__ __forceinline__ int nth_leg(int kap, int idx, int want) {
 //   R2  friction pyramid  -D_rr f_l >= 0                                          (cpp:404-424)
 //   R3  torque limits     +-(Mbar_j qdd - Jc_j^T f) >= -tau_max -+ bbar_j          (cpp:495,506,513)
 //   R4/R5 swing rows      +-(Js_j qdd + Js_com a) + s >= +-c'                     (cpp:496-497,507-515)
-__device__ void build_normal(const Prob& P, const QpMap& mp, const wbc_params& pr, int p, double* n, double& b,
-                             bool& is_eq) {
+__device__ void build_normal(const Prob& P, const double (*G)[12], const QpMap& mp, const wbc_params& pr, int p,
+                             double* n, double& b, bool& is_eq) {
     const int kap = mp.kap;
     const int t_fr = mp.neq, t_tq = mp.neq + mp.nfr, t_sw = t_tq + mp.ntq;
     const bool in = p < mp.m;
@@ -1059,28 +1060,17 @@ __device__ void build_normal(const Prob& P, const QpMap& mp, const wbc_params& p
     const double sq = (eq ? 1.0 : 0.0) + ((tq || sw) ? sg : 0.0);
 #pragma unroll
     for (int j = 0; j < 12; ++j) n[j] = sq * row[j];
-    // slot coupling through a (R1 and R4/R5): delta(k,r)/m + (d_l x e_k) . I_c^-1 (d_mm x e_r)
+    // slot part on stance slots: the coupling through a (R1, R4/R5: row 3 l + k of G, set up with
+    // the slot Hessian) and -+ Jbj[3 mm + r][i] (R3); friction faces and swing slacks are unit rows
     const double scp = eq ? 1.0 : (sw ? sg : 0.0);
-    double v[3];
-    {
-        const double dl[3] = {P.d[3 * l], P.d[3 * l + 1], P.d[3 * l + 2]};
-        const double e[3] = {k == 0 ? 1.0 : 0.0, k == 1 ? 1.0 : 0.0, k == 2 ? 1.0 : 0.0};
-        double u[3];
-        cross3(dl, e, u);
-        mv3(P.Icinv, u, v);
-    }
-    // torque rows: slot of stance leg mm = -+ Jbj[3 mm + r][i] (column i)
     const double stq = tq ? -sg : 0.0;
+    const double* grow = G[3 * l + k];
 #pragma unroll
     for (int mm = 0; mm < 4; ++mm) {
         const bool st = (kap >> mm) & 1;
-        const double dm[3] = {P.d[3 * mm], P.d[3 * mm + 1], P.d[3 * mm + 2]};
-        double vx[3];
-        cross3(v, dm, vx);  // (d_mm x e_r) . v = e_r . (v x d_mm)
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
-            double x = 0.0;
-            if (st) x = scp * (((k == r) ? P.inv_m : 0.0) + vx[r]) + stq * P.Jbj[(3 * mm + r) * 12 + i];
+            double x = st ? fma(scp, grow[3 * mm + r], stq * P.Jbj[(3 * mm + r) * 12 + i]) : 0.0;
             // friction face rr of stance leg l: (-1 | 1 | 0, 0 | 0 | -1 | 1, mu)
             const double fv = (r == 0) ? ((rr == 0) ? -1.0 : (rr == 1 ? 1.0 : 0.0))
                             : (r == 1) ? ((rr == 2) ? -1.0 : (rr == 3 ? 1.0 : 0.0)) : pr.friction;
@@ -1299,6 +1289,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
             mv3(P.Icinv, t, t2);
             Gu[0] = ui[0] + t2[0]; Gu[1] = ui[1] + t2[1]; Gu[2] = ui[2] + t2[2];
             const double ims = 1.0 + inv_m * inv_m;
+            double grow[12];  // row i of G = Jc_com Mbar_b^-1 Jc_com^T (unmasked; the normals mask it)
 #pragma unroll
             for (int j = 0; j < 12; ++j) {
                 const int lj = j / 3, rj = j % 3;
@@ -1308,6 +1299,11 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
                 cross3(dj, ej, uj);
                 const double h = (i == j ? 1.0 : 0.0) + (ri == rj ? ims : 0.0) + dot3(Gu, uj);
                 hrow[j] = (sti && stj) ? h : ((!sti && i == j) ? pr.slack_weight : 0.0);
+                grow[j] = (ri == rj ? inv_m : 0.0) + dot3(t, uj);
+            }
+            if (lane < 12) {
+#pragma unroll
+                for (int j = 0; j < 12; j += 2) *reinterpret_cast<double2*>(&s.G[i][j]) = make_double2(grow[j], grow[j + 1]);
             }
             // g_s = -Jc_com (W + [0, 0, g/m, 0, 0, 0])
             gsv = sti ? -(P.W[ri] + (ri == 2 ? pr.gravity * inv_m : 0.0) + dot3(ui, &P.W[3])) : 0.0;
@@ -1380,7 +1376,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
     const bool is_con = lane < mp.m;
     {
         EST(a, rb, 5);
-        build_normal(P, mp, pr, lane, cc, bp, is_eq);
+        build_normal(P, s.G, mp, pr, lane, cc, bp, is_eq);
         EST(a, rb, 6);
         double np[4] = {0.0, 0.0, 0.0, 0.0}, sq[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -1742,17 +1738,22 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
     // component i from the stored initial columns); qdd part: y = w'; slots: y_s = xs + L^-T w'_s
     double wi = 0.0;
     {
+        // slots in groups of four under a uniform guard: the four column reads of a group are
+        // independent (slots >= q have u = 0 and act = -1 -> column 0, a zero term)
         const int i = lane < NQ ? lane : 0;
-        double w0 = 0.0, w1 = 0.0;  // two chains (even / odd slots)
-        for (int k = 0; k < q; k += 2) {
-            const double2 c = s.c0[i >> 1][bcast_i(act, k)];
-            w0 += bcast(u, k) * ((i & 1) ? c.y : c.x);
-            if (k + 1 < q) {
-                const double2 c1 = s.c0[i >> 1][bcast_i(act, k + 1)];
-                w1 += bcast(u, k + 1) * ((i & 1) ? c1.y : c1.x);
+        double w4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k0 = 0; k0 < NQ; k0 += 4) {
+            if (k0 < q) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int ak = bcast_i(act, k0 + j);
+                    const double2 c = s.c0[i >> 1][ak < 0 ? 0 : ak];
+                    w4[j] = fma(bcast(u, k0 + j), (i & 1) ? c.y : c.x, w4[j]);
+                }
             }
         }
-        wi = lane < NQ ? w0 + w1 : 0.0;
+        wi = lane < NQ ? (w4[0] + w4[1]) + (w4[2] + w4[3]) : 0.0;
     }
     double yv;
     {   // y_s = xs + M^T w'_s (lane i < 12: column i of M, w'_{12 + k} broadcast)
@@ -1769,7 +1770,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
     STAMP(a, rb, 5);
     // outputs: x (42, cpp:534-541), grf = x[18:30] (cpp:556-563), tau (cpp:565-576)
     const bool ok = (status == WBC_QP_OK);
-    if (lane < 42) {
+    if (a.x && lane < 42) {
         double xv;
         if (lane < 6) {  // a = Mbar_b^-1 (Jc_com^T f - gw)
             double F[3] = {0, 0, 0}, Mm[3] = {0, 0, 0};
@@ -1798,7 +1799,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
             const int i = lane - 30;
             xv = ((kap >> (i / 3)) & 1) ? fabs(P.rsw[i]) : yq[12 + i];
         }
-        if (a.x) a.x[(size_t)rb * WBC_NV + lane] = ok ? xv : 0.0;
+        a.x[(size_t)rb * WBC_NV + lane] = ok ? xv : 0.0;
     }
     if (lane < 12) {
         double tv = P.bbj[lane];
