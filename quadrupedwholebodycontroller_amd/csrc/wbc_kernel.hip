@@ -1423,16 +1423,23 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
         bool redundant = false;
         int e0 = 0;
         // fast path, fully unrolled: while no equality has been redundant, equality e goes to slot
-        // q = e, so every row mask below is a compile-time constant
+        // q = e, so every row mask below is a compile-time constant.
+        // tn = |cc[e:]|^2, the tail norm of the lane's own column: lane e's is |d2|^2, so the
+        // reflector scalars start while the column itself is being broadcast (v_readlane).  The
+        // reflection keeps |cc[e:]|, so the next tail is tn - cc[e]^2 (one FMA instead of a 24 - e
+        // term sum); when that cancels (below 2^-10 of tn) on a lane that can still be a pivot, the
+        // tails are summed afresh.
+        double tn;
+        {
+            double zp[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) zp[k & 3] += cc[k] * cc[k];
+            tn = (zp[0] + zp[1]) + (zp[2] + zp[3]);
+        }
 #pragma unroll
         for (int e = 0; e < 12; ++e) {
             if (e < mp.neq && q == e) {
-                // every lane forms the tail norm of its own column; lane e's is |d2|^2, so the
-                // reflector scalars start while the column itself is being broadcast (v_readlane)
-                double zp[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                for (int k = e; k < NQ; ++k) zp[k & 3] += cc[k] * cc[k];
-                const double zn = bcast((zp[0] + zp[1]) + (zp[2] + zp[3]), e);
+                const double zn = bcast(tn, e);
                 double d[NQ];
 #if WBC_EQ_BCAST_LDS
                 // column broadcast through LDS: lane e writes rows e.., every lane reads them back
@@ -1465,6 +1472,17 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
                     const double vw = add ? ((vp[0] + vp[1]) + (vp[2] + vp[3])) * beta : 0.0;
 #pragma unroll
                     for (int k = e; k < NQ; ++k) cc[k] -= vw * d[k];
+                }
+                if (e + 1 < 12) {
+                    const double tr = fma(-cc[e], cc[e], tn);
+                    if (wave_any(lane > e && lane < mp.neq && !(tr >= 0x1p-10 * tn))) {
+                        double zp[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                        for (int k = e + 1; k < NQ; ++k) zp[k & 3] += cc[k] * cc[k];
+                        tn = (zp[0] + zp[1]) + (zp[2] + zp[3]);
+                    } else {
+                        tn = tr;
+                    }
                 }
                 if (add) {
                     if (lane == e) { act = e; myslot = e; }
