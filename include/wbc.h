@@ -196,6 +196,16 @@ int32_t wbc_synchronize(wbc_engine* h);
 int32_t wbc_set_modes(wbc_engine* h, int32_t n_modes, const uint8_t* modes);
 int32_t wbc_step_modes(wbc_engine* h, uint32_t flags);
 
+/* One synchronous control cycle, host arrays in and out (the low-latency path for small batches,
+ * e.g. the B = 1 drop-in of whole_body_controller_node): the inputs are packed into pinned staging
+ * and sent in one H2D copy, the step runs (flags as wbc_step), and the outputs come back in one D2H
+ * copy and one synchronize.  Same results as wbc_set_state + wbc_set_reference + wbc_step +
+ * wbc_get_output.  Inputs are all required; any output may be NULL (x NULL also skips computing
+ * it, as WBC_NO_X).  Refused while mode hypotheses are set. */
+int32_t wbc_cycle(wbc_engine* h, const double* base_pose, const double* nu, const double* qj, const double* ref,
+                  const uint8_t* contacts, const uint8_t* switching, uint32_t flags, double* tau, double* grf,
+                  double* x, int32_t* status, int32_t* iters);
+
 /* Outputs (host copies, synchronous).  Any pointer may be NULL.
  * tau [B][12], grf [B][12] (= x[18:30]), x [B][42], status [B], iters [B]. */
 int32_t wbc_get_output(wbc_engine* h, double* tau, double* grf, double* x, int32_t* status,

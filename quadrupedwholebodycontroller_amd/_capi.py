@@ -26,7 +26,7 @@ DBG = dict(COM=0, COMVEL=3, POSE=6, VC=12, M=18, CNU=342, JFEET=360, PFEET=576, 
 C_API_SYMBOLS = [
     "wbc_default_params", "wbc_anymal_model", "wbc_create", "wbc_destroy", "wbc_batch", "wbc_set_stream",
     "wbc_set_state", "wbc_set_reference", "wbc_bind_device_inputs", "wbc_bind_device_outputs", "wbc_reset", "wbc_update", "wbc_solve",
-    "wbc_step", "wbc_set_modes", "wbc_step_modes", "wbc_synchronize", "wbc_get_output", "wbc_device_outputs", "wbc_get_debug", "wbc_last_kernel_ms",
+    "wbc_step", "wbc_set_modes", "wbc_step_modes", "wbc_cycle", "wbc_synchronize", "wbc_get_output", "wbc_device_outputs", "wbc_get_debug", "wbc_last_kernel_ms",
     "wbc_last_error", "wbc_model_from_urdf",
 ]
 
@@ -86,6 +86,7 @@ def load_library(path: str = LIB_PATH):
         "wbc_solve": ([P, U32], I32),
         "wbc_step": ([P, U32], I32),
         "wbc_set_modes": ([P, I32, P], I32),
+        "wbc_cycle": ([P, P, P, P, P, P, P, U32, P, P, P, P, P], I32),
         "wbc_step_modes": ([P, U32], I32),
         "wbc_synchronize": ([P], I32),
         "wbc_get_output": ([P, P, P, P, P, P], I32),
@@ -215,6 +216,18 @@ class Engine:
 
     def step(self, flags: int = 0):
         self._check(self.lib.wbc_step(self.h, flags), "wbc_step")
+
+    def cycle(self, base_pose, nu, qj, ref, contacts, switching, flags: int = 0, want_x: bool = True):
+        """wbc_cycle: one synchronous host-to-host control cycle (one H2D copy, the step, one D2H copy)."""
+        B = self.batch
+        f = lambda v, n: np.ascontiguousarray(v, np.float64).reshape(B, n)
+        ins = [f(base_pose, POSE_LEN), f(nu, NU_LEN), f(qj, NUM_JOINTS), f(ref, REF_LEN),
+               np.ascontiguousarray(contacts, np.uint8).reshape(B), np.ascontiguousarray(switching, np.uint8).reshape(B)]
+        tau = np.zeros((B, NUM_JOINTS)); grf = np.zeros((B, NUM_JOINTS)); x = np.zeros((B, NV)) if want_x else None
+        st = np.zeros(B, np.int32); it = np.zeros(B, np.int32)
+        self._check(self.lib.wbc_cycle(self.h, *[_ptr(a) for a in ins], flags, _ptr(tau), _ptr(grf), _ptr(x), _ptr(st),
+                                       _ptr(it)), "wbc_cycle")
+        return dict(tau=tau, grf=grf, x=x, status=st, iters=it)
 
     def set_modes(self, modes=None):
         """wbc_set_modes: solve every state under each contact mask in `modes` (None / [] clears)."""

@@ -70,8 +70,9 @@ WbcReferenceMsg make_reference(const double* ref, int contacts) {
     return r;
 }
 
-int run_stance(long cycles, double rate) {
+int run_stance(long cycles, double rate, uint32_t flags) {
     WholeBodyController wbc;
+    wbc.setStepFlags(flags);
     double pose[7] = {0.0, 0.0, 0.585, 0.0, 0.0, 0.0, 1.0};
     double nu[18] = {0};
     const double q0[12] = {0.0, -0.4, 0.8, 0.0, 0.4, -0.8, 0.0, 0.4, -0.8, 0.0, -0.4, 0.8};
@@ -164,9 +165,12 @@ int run_replay(const char* in_path, const char* out_path) {
 int main(int argc, char** argv) {
     try {
         const std::string mode = argc > 1 ? argv[1] : "stance";
-        if (mode == "stance") return run_stance(argc > 2 ? std::atol(argv[2]) : 1000, argc > 3 ? std::atof(argv[3]) : 0.0);
+        if (mode == "stance")
+            return run_stance(argc > 2 ? std::atol(argv[2]) : 1000, argc > 3 ? std::atof(argv[3]) : 0.0,
+                              (argc > 4 && std::string(argv[4]) == "fused") ? WBC_FUSED
+                              : (argc > 4 && std::string(argv[4]) == "split") ? WBC_SPLIT : WBC_FUSED);
         if (mode == "replay" && argc > 3) return run_replay(argv[2], argv[3]);
-        std::fprintf(stderr, "usage: %s stance [cycles] [rate_hz] | replay <in.bin> <out.bin>\n", argv[0]);
+        std::fprintf(stderr, "usage: %s stance [cycles] [rate_hz] [fused|split] | replay <in.bin> <out.bin>\n", argv[0]);
         return 2;
     } catch (const std::exception& e) {
         std::fprintf(stderr, "wbc_control_loop: %s\n", e.what());

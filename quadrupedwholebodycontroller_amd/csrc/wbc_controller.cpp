@@ -135,6 +135,24 @@ void WholeBodyController::computeJointTorques() {
     check(wbc_get_output(engine_, tau_.data(), grf_.data(), x_.data(), &st, &it), "wbc_get_output");
     qpStatus_ = st;
     qpIters_ = it;
+    publish();
+}
+
+void WholeBodyController::controlCycle() {
+    uint8_t contacts = 0;
+    for (int i = 0; i < numberOfLegs; ++i) contacts |= (uint8_t)(footContacts_[i] ? 1u << i : 0u);
+    const uint8_t sw = isSwitchingFootState_ ? 1 : 0;
+    int32_t st = 0, it = 0;
+    check(wbc_cycle(engine_, basePose_, nu_, jointPos_, ref_, &contacts, &sw, stepFlags_, tau_.data(), grf_.data(), x_.data(),
+                    &st, &it),
+          "wbc_cycle");
+    firstControllerIteration_ = false;
+    qpStatus_ = st;
+    qpIters_ = it;
+    publish();
+}
+
+void WholeBodyController::publish() {
     // published before the caller checks the QP status, as in the reference (cpp:652-659)
     if (desiredGroundReactionForcesPublisher) {
         Float64MultiArray g;
@@ -164,9 +182,7 @@ long WholeBodyController::controlLoop(long max_iterations, double rate_hz, const
     long iteration = 0;
     for (; iteration < max_iterations; ++iteration) {
         if (beforeCycle) beforeCycle(iteration);
-        updateState();
-        solveQP();
-        computeJointTorques();
+        controlCycle();  // updateState(); solveQP(); computeJointTorques();
         if (qpStatus_ != WBC_QP_OK) {  // cpp:654-659
             terminate();
             ++iteration;

@@ -40,7 +40,12 @@ struct wbc_engine {
     hipStream_t stream = nullptr;
     wbc_model* d_model = nullptr;
     wbc_params* d_params = nullptr;
-    // owned inputs
+    // owned inputs: one device block [pose | nu | qj | ref | contacts | switching] (so a host cycle
+    // is one H2D copy), and the outputs one block [tau | grf | status | iters | x]
+    void* d_inblk = nullptr;
+    void* d_outblk = nullptr;
+    void* h_in = nullptr;   // pinned staging of the same layouts (wbc_cycle, allocated on first use)
+    void* h_out = nullptr;
     double* d_pose = nullptr;
     double* d_nu = nullptr;
     double* d_qj = nullptr;
@@ -83,6 +88,14 @@ namespace {
 template <class T>
 hipError_t dalloc(T** p, size_t n) {
     return hipMalloc(reinterpret_cast<void**>(p), sizeof(T) * (n ? n : 1));
+}
+
+// device input / output block sizes (bytes)
+size_t in_block_bytes(size_t B) {
+    return B * (WBC_POSE_LEN + WBC_NU_LEN + WBC_NUM_JOINTS + WBC_REF_LEN) * sizeof(double) + 2 * B;
+}
+size_t out_block_bytes(size_t B) {
+    return B * 2 * WBC_NUM_JOINTS * sizeof(double) + 2 * B * sizeof(int32_t) + B * WBC_NV * sizeof(double);
 }
 
 // rows of the input arrays: one per robot, or one per state when mode hypotheses are set
@@ -171,21 +184,29 @@ int32_t wbc_create(const wbc_model* model, const wbc_params* params, int32_t bat
     }
     ALLOC(d_model, 1);
     ALLOC(d_params, 1);
-    ALLOC(d_pose, B * WBC_POSE_LEN);
-    ALLOC(d_nu, B * WBC_NU_LEN);
-    ALLOC(d_qj, B * WBC_NUM_JOINTS);
-    ALLOC(d_ref, B * WBC_REF_LEN);
-    ALLOC(d_contacts, B);
-    ALLOC(d_switching, B);
+    if (hipMalloc(&h->d_inblk, in_block_bytes(B)) != hipSuccess || hipMalloc(&h->d_outblk, out_block_bytes(B)) != hipSuccess) {
+        wbc_destroy(h);
+        return fail(WBC_ERR_HIP, "hipMalloc failed: input/output blocks");
+    }
+    {
+        double* in = static_cast<double*>(h->d_inblk);
+        h->d_pose = in;
+        h->d_nu = h->d_pose + B * WBC_POSE_LEN;
+        h->d_qj = h->d_nu + B * WBC_NU_LEN;
+        h->d_ref = h->d_qj + B * WBC_NUM_JOINTS;
+        h->d_contacts = reinterpret_cast<uint8_t*>(h->d_ref + B * WBC_REF_LEN);
+        h->d_switching = h->d_contacts + B;
+        double* out = static_cast<double*>(h->d_outblk);
+        h->d_tau = out;
+        h->d_grf = h->d_tau + B * WBC_NUM_JOINTS;
+        h->d_status = reinterpret_cast<int32_t*>(h->d_grf + B * WBC_NUM_JOINTS);
+        h->d_iters = h->d_status + B;
+        h->d_x = reinterpret_cast<double*>(h->d_iters + B);  // status + iters = 8 B per robot: aligned
+    }
     ALLOC(d_mask, B);
     ALLOC(d_modes, WBC_MAX_MODES);
     ALLOC(d_hist, B * wbc::HIST_LEN);
     ALLOC(d_work, B * wbc::PROB_LEN);
-    ALLOC(d_tau, B * WBC_NUM_JOINTS);
-    ALLOC(d_grf, B * WBC_NUM_JOINTS);
-    ALLOC(d_x, B * WBC_NV);
-    ALLOC(d_status, B);
-    ALLOC(d_iters, B);
     ALLOC(d_dbg, B * WBC_DBG_LEN);
 #undef ALLOC
     if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess ||
@@ -232,10 +253,12 @@ int32_t wbc_destroy(wbc_engine* h) {
     if (!h) return WBC_OK;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
-    void* ptrs[] = {h->d_model, h->d_params, h->d_pose, h->d_nu, h->d_qj, h->d_ref, h->d_contacts, h->d_switching,
-                    h->d_mask, h->d_modes, h->d_hist, h->d_work, h->d_tau, h->d_grf, h->d_x, h->d_status, h->d_iters, h->d_dbg};
+    void* ptrs[] = {h->d_model, h->d_params, h->d_inblk, h->d_outblk, h->d_mask, h->d_modes, h->d_hist, h->d_work,
+                    h->d_dbg};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    if (h->h_in) (void)hipHostFree(h->h_in);
+    if (h->h_out) (void)hipHostFree(h->h_out);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
@@ -389,6 +412,60 @@ int32_t wbc_step_modes(wbc_engine* h, uint32_t flags) {
         h->timed = true;
     }
     h->updated = false;
+    return WBC_OK;
+}
+
+int32_t wbc_cycle(wbc_engine* h, const double* base_pose, const double* nu, const double* qj, const double* ref,
+                  const uint8_t* contacts, const uint8_t* switching, uint32_t flags, double* tau, double* grf, double* x,
+                  int32_t* status, int32_t* iters) {
+    if (!h) return fail(WBC_ERR_ARG, "null handle");
+    if (h->n_modes) return fail(WBC_ERR_STATE, "wbc_cycle: mode hypotheses are set");
+    if (!base_pose || !nu || !qj || !ref || !contacts || !switching) return fail(WBC_ERR_ARG, "wbc_cycle: null input");
+    WBC_HIP(hipSetDevice(h->device));
+    const size_t B = (size_t)h->batch;
+    const size_t inb = in_block_bytes(B), outb = out_block_bytes(B);
+    if (!h->h_in) {
+        WBC_HIP(hipHostMalloc(&h->h_in, inb, hipHostMallocDefault));
+        WBC_HIP(hipHostMalloc(&h->h_out, outb, hipHostMallocDefault));
+    }
+    // pack the host inputs in the device block's layout (pinned), one H2D copy
+    double* hp = static_cast<double*>(h->h_in);
+    std::memcpy(hp, base_pose, B * WBC_POSE_LEN * sizeof(double));
+    hp += B * WBC_POSE_LEN;
+    std::memcpy(hp, nu, B * WBC_NU_LEN * sizeof(double));
+    hp += B * WBC_NU_LEN;
+    std::memcpy(hp, qj, B * WBC_NUM_JOINTS * sizeof(double));
+    hp += B * WBC_NUM_JOINTS;
+    std::memcpy(hp, ref, B * WBC_REF_LEN * sizeof(double));
+    hp += B * WBC_REF_LEN;
+    std::memcpy(reinterpret_cast<uint8_t*>(hp), contacts, B);
+    std::memcpy(reinterpret_cast<uint8_t*>(hp) + B, switching, B);
+    WBC_HIP(hipMemcpyAsync(h->d_inblk, h->h_in, inb, hipMemcpyHostToDevice, h->stream));
+    h->in_pose = h->d_pose;
+    h->in_nu = h->d_nu;
+    h->in_qj = h->d_qj;
+    h->in_ref = h->d_ref;
+    h->in_contacts = h->d_contacts;
+    h->in_switching = h->d_switching;
+    // outputs into the engine's own block (caller bindings are restored afterwards)
+    double* const bt = h->out_tau; double* const bg = h->out_grf; double* const bx = h->out_x;
+    int32_t* const bs = h->out_status; int32_t* const bi = h->out_iters;
+    h->out_tau = h->d_tau; h->out_grf = h->d_grf; h->out_x = h->d_x; h->out_status = h->d_status; h->out_iters = h->d_iters;
+    if (!x) flags |= WBC_NO_X;
+    const int32_t rc = wbc_step(h, flags);
+    h->out_tau = bt; h->out_grf = bg; h->out_x = bx; h->out_status = bs; h->out_iters = bi;
+    if (rc != WBC_OK) return rc;
+    // one D2H copy (x, last in the block, only when asked for)
+    const size_t xb = B * WBC_NV * sizeof(double);
+    WBC_HIP(hipMemcpyAsync(h->h_out, h->d_outblk, x ? outb : outb - xb, hipMemcpyDeviceToHost, h->stream));
+    WBC_HIP(hipStreamSynchronize(h->stream));
+    const double* o = static_cast<const double*>(h->h_out);
+    if (tau) std::memcpy(tau, o, B * WBC_NUM_JOINTS * sizeof(double));
+    if (grf) std::memcpy(grf, o + B * WBC_NUM_JOINTS, B * WBC_NUM_JOINTS * sizeof(double));
+    const int32_t* oi = reinterpret_cast<const int32_t*>(o + 2 * B * WBC_NUM_JOINTS);
+    if (status) std::memcpy(status, oi, B * sizeof(int32_t));
+    if (iters) std::memcpy(iters, oi + B, B * sizeof(int32_t));
+    if (x) std::memcpy(x, reinterpret_cast<const double*>(oi + 2 * B), xb);
     return WBC_OK;
 }
 

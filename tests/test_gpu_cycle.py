@@ -1,0 +1,65 @@
+"""GPU: wbc_cycle, the one-call host-to-host control cycle (pinned staging, one H2D copy, the
+step, one D2H copy).  It must give exactly what wbc_set_state + wbc_set_reference + wbc_step +
+wbc_get_output give, cold and stateful, for odd batch sizes (output block alignment), with and
+without x, and leave caller-bound output buffers bound."""
+import numpy as np
+import pytest
+
+from quadrupedwholebodycontroller_amd import STATELESS, Engine, WbcError, workloads
+
+pytestmark = pytest.mark.gpu
+
+KEYS = ("tau", "grf", "x", "status", "iters")
+
+
+def separate_calls(e, inp, flags):
+    e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
+    e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
+    e.step(flags)
+    return e.outputs()
+
+
+@pytest.mark.parametrize("B", [1, 33, 256])
+def test_cycle_equals_separate_calls_cold(B):
+    inp = workloads.rl_random(B, seed=40 + B)
+    e1, e2 = Engine(B), Engine(B)
+    want = separate_calls(e1, inp, STATELESS)
+    got = e2.cycle(inp["base_pose"], inp["nu"], inp["qj"], inp["ref"], inp["contacts"], inp["switching"], STATELESS)
+    no_x = e2.cycle(inp["base_pose"], inp["nu"], inp["qj"], inp["ref"], inp["contacts"], inp["switching"], STATELESS,
+                    want_x=False)
+    e1.close(); e2.close()
+    for k in KEYS:
+        assert np.array_equal(got[k], want[k]), k
+    for k in ("tau", "grf", "status", "iters"):
+        assert np.array_equal(no_x[k], want[k]), k
+
+
+def test_cycle_equals_separate_calls_stateful_trot():
+    B, T = 48, 60
+    seq = list(workloads.trot_sequence(B, steps=T, seed=5))
+    e1, e2 = Engine(B), Engine(B)
+    for t, s in enumerate(seq):
+        want = separate_calls(e1, s, 0)
+        got = e2.cycle(s["base_pose"], s["nu"], s["qj"], s["ref"], s["contacts"], s["switching"], 0)
+        for k in KEYS:
+            assert np.array_equal(got[k], want[k]), (t, k)
+    e1.close(); e2.close()
+
+
+def test_cycle_keeps_bound_outputs_and_refuses_modes():
+    import torch
+
+    B = 16
+    inp = workloads.stance_cold(B, seed=41)
+    e = Engine(B)
+    tau_dev = torch.zeros(B * 12, dtype=torch.float64, device="cuda")
+    e.bind_device_outputs(tau=tau_dev.data_ptr())
+    got = e.cycle(inp["base_pose"], inp["nu"], inp["qj"], inp["ref"], inp["contacts"], inp["switching"], STATELESS)
+    # the cycle returns its own copy; the bound tensor stays bound for the next plain step
+    e.step(STATELESS)
+    torch.cuda.synchronize()
+    assert np.array_equal(tau_dev.cpu().numpy().reshape(B, 12), got["tau"])
+    e.set_modes([15, 5])
+    with pytest.raises(WbcError):
+        e.cycle(inp["base_pose"], inp["nu"], inp["qj"], inp["ref"], inp["contacts"], inp["switching"], STATELESS)
+    e.close()
