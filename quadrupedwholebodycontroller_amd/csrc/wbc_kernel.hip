@@ -1429,6 +1429,13 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
         // reflection keeps |cc[e:]|, so the next tail is tn - cc[e]^2 (one FMA instead of a 24 - e
         // term sum); when that cancels (below 2^-10 of tn) on a lane that can still be a pivot, the
         // tails are summed afresh.
+        // rinv: row `lane` of R^-1, built column by column alongside the reflections
+        // (R^-1 gains [-R^-1 r_e / alpha_e; 1 / alpha_e], r_e = rows < e of column e, final before
+        // step e): an independent chain that overlaps the reflections' latency and replaces the
+        // two 12-step substitutions after the block
+        double rinv[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) rinv[k] = 0.0;
         double tn;
         {
             double zp[4] = {0.0, 0.0, 0.0, 0.0};
@@ -1465,6 +1472,13 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
                     const double nrm2 = zs * rs;
                     const double alpha = (dqs >= 0.0) ? -nrm2 : nrm2;
                     const double beta = fast_rcp(zs + nrm2 * fabs(dqs));
+                    {
+                        const double ia = (dqs >= 0.0) ? -rs : rs;  // 1 / alpha
+                        double rk[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                        for (int k = 0; k < e; ++k) rk[k & 3] = fma(rinv[k], bcast(cc[k], e), rk[k & 3]);
+                        rinv[e] = (lane == e) ? ia : -((rk[0] + rk[1]) + (rk[2] + rk[3])) * ia;
+                    }
                     d[e] = dqs - alpha;
                     double vp[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -1526,6 +1540,27 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
         }
         neq_added = q;
         EST(a, rb, 2);
+        if (!wave_any(redundant)) {
+            // every equality went to slot = lane in the fast path: R^-1 rows are in rinv.
+            // v = -R^-T s_E (uniform): v_j = -sum_k R^-1[k][j] s_k over the slots k < q (lanes
+            // 0..11, one DPP row), u = R^-1 v, s += C[0:q]^T v
+            double v[12];
+#pragma unroll
+            for (int j = 0; j < 12; ++j) v[j] = -row0_sum((lane < q) ? rinv[j] * sp : 0.0);
+            double uu[4] = {0.0, 0.0, 0.0, 0.0}, ds[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int j = 0; j < 12; ++j) {
+                uu[j & 3] = fma(rinv[j], v[j], uu[j & 3]);
+                ds[j & 3] = fma(cc[j], v[j], ds[j & 3]);
+            }
+            if (lane < q) {
+                u = (uu[0] + uu[1]) + (uu[2] + uu[3]);
+#pragma unroll
+                for (int jj = 0; jj < 6; ++jj) s.Rv[jj][lane] = make_double2(rinv[2 * jj], rinv[2 * jj + 1]);
+            }
+            sp += (ds[0] + ds[1]) + (ds[2] + ds[3]);
+            lds_sync();
+        } else {
         // R columns and equality slacks by slot
         if (myslot >= 0) {
 #pragma unroll
@@ -1566,6 +1601,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
         const bool bad = redundant && !(fabs(sp) <= 1e-9 * fmax(1.0, fabs(bp)));
         if (wave_any(bad)) { status = WBC_QP_INFEASIBLE; done = true; }
         lds_sync();
+        }
     }
     EST(a, rb, 4);
 
