@@ -1290,16 +1290,21 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
             Gu[0] = ui[0] + t2[0]; Gu[1] = ui[1] + t2[1]; Gu[2] = ui[2] + t2[2];
             const double ims = 1.0 + inv_m * inv_m;
             double grow[12];  // row i of G = Jc_com Mbar_b^-1 Jc_com^T (unmasked; the normals mask it)
+            // with u_j = d_lj x e_rj: a . u_j = (a x d_lj)[rj], one cross product per leg
 #pragma unroll
-            for (int j = 0; j < 12; ++j) {
-                const int lj = j / 3, rj = j % 3;
+            for (int lj = 0; lj < 4; ++lj) {
                 const bool stj = (kap >> lj) & 1;
                 const double dj[3] = {P.d[3 * lj], P.d[3 * lj + 1], P.d[3 * lj + 2]};
-                double ej[3] = {rj == 0 ? 1.0 : 0.0, rj == 1 ? 1.0 : 0.0, rj == 2 ? 1.0 : 0.0}, uj[3];
-                cross3(dj, ej, uj);
-                const double h = (i == j ? 1.0 : 0.0) + (ri == rj ? ims : 0.0) + dot3(Gu, uj);
-                hrow[j] = (sti && stj) ? h : ((!sti && i == j) ? pr.slack_weight : 0.0);
-                grow[j] = (ri == rj ? inv_m : 0.0) + dot3(t, uj);
+                double hc[3], gc[3];
+                cross3(Gu, dj, hc);
+                cross3(t, dj, gc);
+#pragma unroll
+                for (int rj = 0; rj < 3; ++rj) {
+                    const int j = 3 * lj + rj;
+                    const double h = (i == j ? 1.0 : 0.0) + (ri == rj ? ims : 0.0) + hc[rj];
+                    hrow[j] = (sti && stj) ? h : ((!sti && i == j) ? pr.slack_weight : 0.0);
+                    grow[j] = (ri == rj ? inv_m : 0.0) + gc[rj];
+                }
             }
             if (lane < 12) {
 #pragma unroll
@@ -1319,11 +1324,10 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
             const double lkk = dkk * il;
             if (lane == k) ildv = il;
             hrow[k] = (lane == k) ? lkk : hrow[k] * il;   // L_ik for lanes i > k
+            // trailing update, unmasked: lanes i < j only change their upper triangle, which is
+            // never read (the factor is stored masked below)
 #pragma unroll
-            for (int j = k + 1; j < 12; ++j) {
-                const double ljk = bcast(hrow[k], j);
-                if (lane >= j) hrow[j] -= hrow[k] * ljk;
-            }
+            for (int j = k + 1; j < 12; ++j) hrow[j] = fma(-hrow[k], bcast(hrow[k], j), hrow[j]);
         }
         if (!chol_ok && status == WBC_QP_OK) status = WBC_QP_NUMERIC;
         if (lane < 12) {

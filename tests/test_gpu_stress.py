@@ -1,0 +1,64 @@
+"""GPU stress parity: states and references far outside the benchmark distributions, so that the
+active-set solve runs long working-set sequences with many constraint deletions (Givens drops,
+DESIGN.md 4.2) and reaches the non-OK outcomes.  Checked against the numpy oracle (exact dense
+active set on the reference's 42 x 70 QP): identical QP status on every robot, and x* / tau at
+the tolerances of test_gpu_parity.py on the solved ones.
+
+Inputs: joint angles q0 +- 1.2 rad (knees through straight), base velocities N(0, 2), large
+commanded CoM / swing accelerations, all 16 contact masks, and tighter torque limits
+(max_torque 80, 20 and 6 N m) so that torque rows bind, get dropped and re-added, and at 6 N m
+some QPs are infeasible.
+"""
+import numpy as np
+import pytest
+
+import wbc_np as W
+from quadrupedwholebodycontroller_amd import STATELESS, Engine, default_params, workloads
+
+pytestmark = pytest.mark.gpu
+
+
+def stress_inputs(B, seed):
+    g = np.random.default_rng(seed)
+    inp = workloads.rl_random(B, seed=seed)
+    inp["qj"] = workloads.Q0 + g.uniform(-1.2, 1.2, (B, 12))
+    inp["nu"] = g.normal(0.0, 2.0, (B, 18))
+    inp["ref"][:, 12:18] = g.normal(0.0, 15.0, (B, 6))
+    inp["ref"][:, 42:54] = g.normal(0.0, 40.0, (B, 12))
+    inp["contacts"] = (np.arange(B) % 16).astype(np.uint8)
+    return inp
+
+
+@pytest.mark.parametrize("max_torque,seed", [(80.0, 51), (20.0, 52), (6.0, 53)])
+def test_stress_status_and_solution_match_oracle(max_torque, seed):
+    B = 192
+    inp = stress_inputs(B, seed)
+    p = default_params()
+    p.max_torque = max_torque
+    e = Engine(B, params=p)
+    e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
+    e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
+    e.step(STATELESS)
+    out = e.outputs()
+    e.close()
+    model = W.Model()
+    params = W.default_params()
+    params["max_torque"] = max_torque
+    n_ok = 0
+    for b in range(B):
+        c = W.ReferenceWBC(model, params)
+        c.set_state(inp["base_pose"][b], inp["nu"][b], inp["qj"][b])
+        c.set_reference(inp["ref"][b], [(int(inp["contacts"][b]) >> i) & 1 for i in range(4)], True)
+        c.step()
+        assert out["status"][b] == c.qp_status, (b, int(inp["contacts"][b]), out["status"][b], c.qp_status)
+        if c.qp_status == W.QP_OK:
+            n_ok += 1
+            x = c.qp_solution
+            assert np.max(np.abs(out["x"][b] - x)) <= 1e-8 * (1 + np.max(np.abs(x))), (b, "x")
+            assert np.max(np.abs(out["tau"][b] - c.tau)) <= 1e-7 * (1 + np.max(np.abs(c.tau))), (b, "tau")
+    # long working-set sequences; at 6 N m some QPs are infeasible (the reference's qpOASES
+    # failure that stops controlLoop, cpp:654-659)
+    assert out["iters"][out["status"] == 0].max() > 15
+    assert n_ok > 0
+    if max_torque < 10.0:
+        assert n_ok < B
