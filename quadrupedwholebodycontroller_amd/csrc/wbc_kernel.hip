@@ -459,7 +459,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
         const bool anybad = seg_any<SUB>(bad);
         if (lane == 0) { P.flags = anybad ? 1.0 : 0.0; P.kappa = (double)kap; }
     }
-    wsync();
+    lds_sync();
     UST(a, rb, 1);
     const double* pB = &s.in[0];
     const double* vB = &s.in[7];
@@ -527,7 +527,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
 #pragma unroll
         for (int i = 0; i < 3; ++i) { f.o[i] = pB[i]; f.w[i] = wB[i]; f.al[i] = 0.0; f.ao[i] = 0.0; f.vo[i] = vB[i]; }
     }
-    wsync();
+    lds_sync();
 
     UST(a, rb, 2);
     // stage B: one lane per body: com, world inertia, com velocity, m a_com, I alpha + w x I w
@@ -575,7 +575,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
                 for (int i = 0; i < 3; ++i) { s.pf[l][i] = pf[i]; s.vf[l][i] = vo[i] + t[i]; }
             }
         }
-        wsync();  // every frame read before the union is overwritten
+        lds_sync();  // every frame read before the union is overwritten
         if (lane < 13) {
             Body& bd = s.bd[lane];
 #pragma unroll
@@ -590,7 +590,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
             c[i] = seg_sum<SUB>(mb * cb[i]);
         }
     }
-    wsync();
+    lds_sync();
     UST(a, rb, 3);
     // foot Jacobian joint columns (getFrameFreeFloatingJacobian rows 0-2, cpp:327-341): a_k x (p_f - o_k)
     if (lane < 12) {
@@ -689,7 +689,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
         }
         s.hj[j] = dot3(aj, hsum);
     }
-    wsync();
+    lds_sync();
     UST(a, rb, 6);
 
 
@@ -711,7 +711,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
                 for (int k = 0; k < 6; ++k) y[k] = bcast(yl, k);
             } else {
                 if (lane < 6) s.yv[lane] = yl;
-                wsync();
+                lds_sync();
 #pragma unroll
                 for (int k = 0; k < 6; ++k) y[k] = s.yv[k];
             }
@@ -831,7 +831,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
         }
         }
     }
-    wsync();  // all reads of the old history done
+    stateful ? wsync() : lds_sync();  // all reads of the old history done
     if (stateful && wr) {
 #pragma unroll
         for (int it = 0; it < NT; ++it) {
@@ -898,7 +898,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
                  (k == 2 ? md.total_mass * pr.gravity : 0.0) + mba;
         if (stateful && wr) H[H_EINT + k] = eint + e / pr.loop_rate;
     }
-    wsync();
+    stateful ? wsync() : lds_sync();
     if (stateful && wr) {
         for (int k = lane; k < 144; k += SUB) H[H_JBJOLD + k] = P.Jbj[k];
         if (lane < 12) H[H_DOLD + lane] = P.d[lane];
@@ -995,7 +995,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
         }
         for (int e = lane; e < 144; e += SUB) D[WBC_DBG_MBARJ + e] = P.Mbj[e];
     }
-    wsync();
+    lds_sync();
 }
 
 // ---------------------------------------------------------------------------------------
