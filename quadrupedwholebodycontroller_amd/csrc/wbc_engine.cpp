@@ -206,7 +206,7 @@ int32_t wbc_create(const wbc_model* model, const wbc_params* params, int32_t bat
     ALLOC(d_mask, B);
     ALLOC(d_modes, WBC_MAX_MODES);
     ALLOC(d_hist, B * wbc::HIST_LEN);
-    ALLOC(d_work, B * wbc::PROB_LEN);
+    ALLOC(d_work, B * wbc::WORK_LEN);
     ALLOC(d_dbg, B * WBC_DBG_LEN);
 #undef ALLOC
     if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess ||

@@ -50,6 +50,11 @@ struct UpdScratch {
     union {
         Frame fr[13];
         Body bd[13];
+        struct {            // slot factorisation at the end of the update (presolve)
+            double L[12][13];
+            double ild[12];
+            double xs[12];
+        } ps;
     };
     double ja[12][3];       // joint axis (world)
     double jo[12][3];       // joint origin (world)
@@ -126,6 +131,36 @@ __device__ __forceinline__ double dpp_d(double v) {
     int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
     int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
     return __hiloint2double(hi, lo);
+}
+// Lane j (a constant once the caller's loops are unrolled) of the robot's lane segment, to every
+// lane of the segment: v_readlane for one robot per wave, DPP row_newbcast for 16-lane segments
+// (one robot per DPP row: a VALU move, no SGPR round trip, no LDS), ds_bpermute for 32.
+template <int SUB>
+__device__ __forceinline__ double seg_bcast(double v, int j) {
+    if constexpr (SUB == 64) {
+        return bcast(v, j);
+    } else if constexpr (SUB == 16) {
+        switch (j) {
+            case 0: return dpp_d<0x150>(v);
+            case 1: return dpp_d<0x151>(v);
+            case 2: return dpp_d<0x152>(v);
+            case 3: return dpp_d<0x153>(v);
+            case 4: return dpp_d<0x154>(v);
+            case 5: return dpp_d<0x155>(v);
+            case 6: return dpp_d<0x156>(v);
+            case 7: return dpp_d<0x157>(v);
+            case 8: return dpp_d<0x158>(v);
+            case 9: return dpp_d<0x159>(v);
+            case 10: return dpp_d<0x15A>(v);
+            case 11: return dpp_d<0x15B>(v);
+            case 12: return dpp_d<0x15C>(v);
+            case 13: return dpp_d<0x15D>(v);
+            case 14: return dpp_d<0x15E>(v);
+            default: return dpp_d<0x15F>(v);
+        }
+    } else {
+        return vbcast(v, ((int)threadIdx.x & ~(SUB - 1)) + j);
+    }
 }
 template <int CTRL>
 __device__ __forceinline__ int dpp_i(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false); }
@@ -394,6 +429,123 @@ __device__ __forceinline__ double sel3(const double* v, int k) { return k == 0 ?
 #define IST_FLUSH(a, rb) do { } while (0)
 #endif
 
+// Row i (lane i < 12) of the slot coupling G = Jc_com Mbar_b^-1 Jc_com^T (unmasked; the constraint
+// normals mask it).  With u_j = d_lj x e_rj: a . u_j = (a x d_lj)[rj], one cross product per leg.
+__device__ __forceinline__ void g_row(const Prob& P, int i, double* grow) {
+    const int li = i / 3, ri = i % 3;
+    const double di[3] = {P.d[3 * li], P.d[3 * li + 1], P.d[3 * li + 2]};
+    double e[3] = {ri == 0 ? 1.0 : 0.0, ri == 1 ? 1.0 : 0.0, ri == 2 ? 1.0 : 0.0}, ui[3], t[3];
+    cross3(di, e, ui);
+    mv3(P.Icinv, ui, t);
+#pragma unroll
+    for (int lj = 0; lj < 4; ++lj) {
+        const double dj[3] = {P.d[3 * lj], P.d[3 * lj + 1], P.d[3 * lj + 2]};
+        double gc[3];
+        cross3(t, dj, gc);
+#pragma unroll
+        for (int rj = 0; rj < 3; ++rj) grow[3 * lj + rj] = (ri == rj ? P.inv_m : 0.0) + gc[rj];
+    }
+}
+
+// The part of solveQP (cpp:466-515) that depends on the contact mask but not on the constraints:
+// the slot Hessian H_s = I + Jc_com (I + Mbar_b^-2) Jc_com^T on stance slots (slack_weight I on
+// swing slots; lane i < 12 of the robot's segment holds row i), its Cholesky factor, M = L^-1
+// (lower, written over L) and x0's slot part xs = -H_s^-1 g_s.  Runs at the end of the update (four
+// robots per wave in the update kernel) or, under mode hypotheses, in the solve.  Returns false
+// when H_s is not positive definite.
+template <int SUB>
+__device__ bool presolve(const Prob& P, int kap, const wbc_params& pr, int lane, double (&L)[12][13], double* ild,
+                         double* xs) {
+    const double inv_m = P.inv_m;
+    double hrow[12];
+    double gsv = 0.0;
+    {
+        const int i = lane < 12 ? lane : 11, li = i / 3, ri = i % 3;
+        const bool sti = (kap >> li) & 1;
+        const double di[3] = {P.d[3 * li], P.d[3 * li + 1], P.d[3 * li + 2]};
+        double e[3] = {ri == 0 ? 1.0 : 0.0, ri == 1 ? 1.0 : 0.0, ri == 2 ? 1.0 : 0.0}, ui[3];
+        cross3(di, e, ui);
+        double t[3], t2[3], Gu[3];
+        mv3(P.Icinv, ui, t);
+        mv3(P.Icinv, t, t2);
+        Gu[0] = ui[0] + t2[0]; Gu[1] = ui[1] + t2[1]; Gu[2] = ui[2] + t2[2];
+        const double ims = 1.0 + inv_m * inv_m;
+#pragma unroll
+        for (int lj = 0; lj < 4; ++lj) {
+            const bool stj = (kap >> lj) & 1;
+            const double dj[3] = {P.d[3 * lj], P.d[3 * lj + 1], P.d[3 * lj + 2]};
+            double hc[3];
+            cross3(Gu, dj, hc);
+#pragma unroll
+            for (int rj = 0; rj < 3; ++rj) {
+                const int j = 3 * lj + rj;
+                const double h = (i == j ? 1.0 : 0.0) + (ri == rj ? ims : 0.0) + hc[rj];
+                hrow[j] = (sti && stj) ? h : ((!sti && i == j) ? pr.slack_weight : 0.0);
+            }
+        }
+        // g_s = -Jc_com (W + [0, 0, g/m, 0, 0, 0])
+        gsv = sti ? -(P.W[ri] + (ri == 2 ? pr.gravity * inv_m : 0.0) + dot3(ui, &P.W[3])) : 0.0;
+    }
+    // right-looking Cholesky, row i in lane i; L_jk broadcast from lane j of the segment
+    bool chol_ok = true;
+    double ildv = 1.0;  // lane k: 1 / L_kk
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        const double dkk = seg_bcast<SUB>(hrow[k], k);
+        chol_ok &= dkk > 0.0;
+        const double il = fast_rsq(fmax(dkk, 1e-300));
+        const double lkk = dkk * il;
+        if (lane == k) ildv = il;
+        hrow[k] = (lane == k) ? lkk : hrow[k] * il;   // L_ik for lanes i > k
+        // trailing update, unmasked: lanes i < j only change their upper triangle, which is
+        // never read (the factor is stored masked below)
+#pragma unroll
+        for (int j = k + 1; j < 12; ++j) hrow[j] = fma(-hrow[k], seg_bcast<SUB>(hrow[k], j), hrow[j]);
+    }
+    if (lane < 12) {
+#pragma unroll
+        for (int j = 0; j < 12; ++j) L[lane][j] = (j <= lane) ? hrow[j] : 0.0;
+        ild[lane] = ildv;
+    }
+    lds_sync();  // L visible
+    // M = L^-1 (lower triangular), lane j forms column j by forward substitution; every later
+    // use of the factor (C0 = L^-1 n_s, x0, primal recovery) is then a matvec without a chain
+    double (&Mi)[12][12] = *reinterpret_cast<double(*)[12][12]>(&L[0][0]);
+    {
+        double m[12];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+            double a4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int k = 0; k < i; ++k) a4[k & 3] += L[i][k] * m[k];
+            m[i] = (((lane == i) ? 1.0 : 0.0) - ((a4[0] + a4[1]) + (a4[2] + a4[3]))) * ild[i];
+        }
+        lds_sync();  // all reads of L done: M overwrites it
+        if (lane < 12) {
+#pragma unroll
+            for (int i = 0; i < 12; ++i) Mi[i][lane] = (i >= lane) ? m[i] : 0.0;
+        }
+    }
+    lds_sync();
+    // x0 = -H_s^-1 g_s = -M^T (M g_s): g_k and z_k broadcast from lane k
+    {
+        double gk[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) gk[k] = seg_bcast<SUB>(gsv, k);
+        const int i = lane < 12 ? lane : 0;
+        double z4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k = 0; k < 12; ++k) z4[k & 3] += Mi[i][k] * gk[k];
+        const double zi = (z4[0] + z4[1]) + (z4[2] + z4[3]);
+        double x4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k = 0; k < 12; ++k) x4[k & 3] += Mi[k][i] * seg_bcast<SUB>(zi, k);
+        if (lane < 12) xs[lane] = -((x4[0] + x4[1]) + (x4[2] + x4[3]));
+    }
+    lds_sync();
+    return chol_ok;
+}
+
 // ---------------------------------------------------------------------------------------
 // update phase (≙ updateState, cpp:256-294, plus the per-cycle terms of solveQP that do not
 // depend on the QP: computeDesiredWrench cpp:426-445, swing commands cpp:447-464, bounds cpp:503-515)
@@ -402,7 +554,7 @@ __device__ __forceinline__ double sel3(const double* v, int k) { return k == 0 ?
 // own scratch); lane = lane within the robot's segment; wr = false for a padding segment past the
 // batch (computes a duplicate robot, writes nothing to HBM).
 template <int SUB>
-__device__ void update_phase(const KernelArgs& a, int rb, int lane, bool wr, UpdScratch& s, Prob& P) {
+__device__ void update_phase(const KernelArgs& a, int rb, int lane, bool wr, UpdScratch& s, Prob& P, Presolve* pre) {
     const wbc_model& md = *a.model;
     const wbc_params& pr = *a.params;
     const int kap = a.contacts[rb];
@@ -996,6 +1148,27 @@ __device__ void update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
         for (int e = lane; e < 144; e += SUB) D[WBC_DBG_MBARJ + e] = P.Mbj[e];
     }
     lds_sync();
+    // the slot factorisation of the solve's start, here where the robot's own contact mask is
+    // known (not under mode hypotheses, whose masks differ per QP): in the update kernel four
+    // robots share a wave, so this 12-lane work costs a quarter of its one-robot-per-wave price
+    if (pre) {
+        if (!a.modes) {
+            const bool ok = presolve<SUB>(P, kap, pr, lane, s.ps.L, s.ps.ild, s.ps.xs);
+            const double (&Mi)[12][12] = *reinterpret_cast<const double(*)[12][12]>(&s.ps.L[0][0]);
+            for (int k = lane; k < 78; k += SUB) {
+                const int i = (int)((sqrt(8.0 * k + 1.0) - 1.0) * 0.5);
+                pre->Mi[k] = Mi[i][k - i * (i + 1) / 2];
+            }
+            if (lane < 12) pre->xs[lane] = s.ps.xs[lane];
+            if (lane == 0) {
+                pre->presolved = 1.0;
+                if (!ok) P.flags += 2.0;
+            }
+        } else if (lane == 0) {
+            pre->presolved = 0.0;
+        }
+        lds_sync();
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1257,15 +1430,13 @@ __device__ void active_set_point(const QpScratch& s, int q, int act, double sp0,
     sp = sp0 + ((s4[0] + s4[1]) + (s4[2] + s4[3]));
 }
 
-__device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratch& s) {
+__device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, const Presolve* pre, QpScratch& s) {
     const wbc_params& pr = *a.params;
     const int lane = lane_id();
     const int kap = (int)P.kappa;
     const QpMap mp = make_map(kap);
     int status = WBC_QP_OK;
     int iters = 0;
-    const double inv_m = P.inv_m;
-
     if (P.flags != 0.0) status = WBC_QP_NUMERIC;
     {   // vacuous rows (quirk A.12): swing-leg rows of R1 read 0 = r1
         bool bad = false;
@@ -1273,102 +1444,22 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
         if (wave_any(bad) && status == WBC_QP_OK) status = WBC_QP_INFEASIBLE;
     }
 
-    // slot Hessian H_s = I + Jc_com (I + Mbar_b^-2) Jc_com^T on stance slots, slack_weight I on
-    // swing slots (lane i holds row i), its Cholesky factor in registers, x0 = -H^-1 g
-    {
-        double hrow[12];
-        double gsv = 0.0;
-        {
-            const int i = lane < 12 ? lane : 11, li = i / 3, ri = i % 3;
-            const bool sti = (kap >> li) & 1;
-            const double di[3] = {P.d[3 * li], P.d[3 * li + 1], P.d[3 * li + 2]};
-            double e[3] = {ri == 0 ? 1.0 : 0.0, ri == 1 ? 1.0 : 0.0, ri == 2 ? 1.0 : 0.0}, ui[3];
-            cross3(di, e, ui);
-            double t[3], t2[3], Gu[3];
-            mv3(P.Icinv, ui, t);
-            mv3(P.Icinv, t, t2);
-            Gu[0] = ui[0] + t2[0]; Gu[1] = ui[1] + t2[1]; Gu[2] = ui[2] + t2[2];
-            const double ims = 1.0 + inv_m * inv_m;
-            double grow[12];  // row i of G = Jc_com Mbar_b^-1 Jc_com^T (unmasked; the normals mask it)
-            // with u_j = d_lj x e_rj: a . u_j = (a x d_lj)[rj], one cross product per leg
+    // slot coupling rows; the slot factor M = L^-1 and x0 come from the update (packed into the
+    // problem) unless the contact mask is this QP's own (mode hypotheses): then formed here
+    if (lane < 12) {
+        double grow[12];
+        g_row(P, lane, grow);
 #pragma unroll
-            for (int lj = 0; lj < 4; ++lj) {
-                const bool stj = (kap >> lj) & 1;
-                const double dj[3] = {P.d[3 * lj], P.d[3 * lj + 1], P.d[3 * lj + 2]};
-                double hc[3], gc[3];
-                cross3(Gu, dj, hc);
-                cross3(t, dj, gc);
-#pragma unroll
-                for (int rj = 0; rj < 3; ++rj) {
-                    const int j = 3 * lj + rj;
-                    const double h = (i == j ? 1.0 : 0.0) + (ri == rj ? ims : 0.0) + hc[rj];
-                    hrow[j] = (sti && stj) ? h : ((!sti && i == j) ? pr.slack_weight : 0.0);
-                    grow[j] = (ri == rj ? inv_m : 0.0) + gc[rj];
-                }
-            }
-            if (lane < 12) {
-#pragma unroll
-                for (int j = 0; j < 12; j += 2) *reinterpret_cast<double2*>(&s.G[i][j]) = make_double2(grow[j], grow[j + 1]);
-            }
-            // g_s = -Jc_com (W + [0, 0, g/m, 0, 0, 0])
-            gsv = sti ? -(P.W[ri] + (ri == 2 ? pr.gravity * inv_m : 0.0) + dot3(ui, &P.W[3])) : 0.0;
+        for (int j = 0; j < 12; j += 2) *reinterpret_cast<double2*>(&s.G[lane][j]) = make_double2(grow[j], grow[j + 1]);
+    }
+    if (pre && pre->presolved != 0.0) {
+        for (int k = lane; k < 144; k += 64) {
+            const int i = k / 12, j = k % 12;
+            s.Mi()[i][j] = (j <= i) ? pre->Mi[i * (i + 1) / 2 + j] : 0.0;
         }
-        // right-looking Cholesky, row i in lane i; L_jk broadcast with v_readlane
-        bool chol_ok = true;
-        double ildv = 1.0;  // lane k: 1 / L_kk
-#pragma unroll
-        for (int k = 0; k < 12; ++k) {
-            const double dkk = bcast(hrow[k], k);
-            chol_ok &= dkk > 0.0;
-            const double il = fast_rsq(fmax(dkk, 1e-300));
-            const double lkk = dkk * il;
-            if (lane == k) ildv = il;
-            hrow[k] = (lane == k) ? lkk : hrow[k] * il;   // L_ik for lanes i > k
-            // trailing update, unmasked: lanes i < j only change their upper triangle, which is
-            // never read (the factor is stored masked below)
-#pragma unroll
-            for (int j = k + 1; j < 12; ++j) hrow[j] = fma(-hrow[k], bcast(hrow[k], j), hrow[j]);
-        }
-        if (!chol_ok && status == WBC_QP_OK) status = WBC_QP_NUMERIC;
-        if (lane < 12) {
-#pragma unroll
-            for (int j = 0; j < 12; ++j) s.L[lane][j] = (j <= lane) ? hrow[j] : 0.0;
-            s.ild[lane] = ildv;
-        }
-        lds_sync();  // L visible
-        // M = L^-1 (lower triangular), lane j forms column j by forward substitution; every later
-        // use of the factor (C0 = L^-1 n_s, x0, primal recovery) is then a matvec without a chain
-        {
-            double m[12];
-#pragma unroll
-            for (int i = 0; i < 12; ++i) {
-                double a4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                for (int k = 0; k < i; ++k) a4[k & 3] += s.L[i][k] * m[k];
-                m[i] = (((lane == i) ? 1.0 : 0.0) - ((a4[0] + a4[1]) + (a4[2] + a4[3]))) * s.ild[i];
-            }
-            lds_sync();  // all reads of L done: M overwrites it
-            if (lane < 12) {
-#pragma unroll
-                for (int i = 0; i < 12; ++i) s.Mi()[i][lane] = (i >= lane) ? m[i] : 0.0;
-            }
-        }
-        lds_sync();
-        // x0 = -H_s^-1 g_s = -M^T (M g_s): g_k and z_k broadcast from lane k
-        {
-            double gk[12];
-#pragma unroll
-            for (int k = 0; k < 12; ++k) gk[k] = bcast(gsv, k);
-            const int i = lane < 12 ? lane : 0;
-            double z4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int k = 0; k < 12; ++k) z4[k & 3] += s.Mi()[i][k] * gk[k];
-            const double zi = (z4[0] + z4[1]) + (z4[2] + z4[3]);
-            double x4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int k = 0; k < 12; ++k) x4[k & 3] += s.Mi()[k][i] * bcast(zi, k);
-            if (lane < 12) s.xs[lane] = -((x4[0] + x4[1]) + (x4[2] + x4[3]));
-        }
+        if (lane < 12) s.xs[lane] = pre->xs[lane];
+    } else if (!presolve<64>(P, kap, pr, lane, s.L, s.ild, s.xs) && status == WBC_QP_OK) {
+        status = WBC_QP_NUMERIC;
     }
     lds_sync();
 
@@ -1911,6 +2002,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, QpScratc
 constexpr int UPD_SUB = WBC_UPDATE_SUB, UPD_RPW = 64 / UPD_SUB;
 struct UpdLds {
     Prob prob[UPD_RPW];
+    Presolve pre[UPD_RPW];
     UpdScratch u[UPD_RPW];
 };
 struct SolveLds {
@@ -1923,9 +2015,9 @@ WBC_KERNEL_ATTR void wbc_step_kernel(KernelArgs a) {
     const int rb = xcd_robot();
     if (rb >= a.batch) return;
     STAMP(a, rb, 0);
-    update_phase<64>(a, rb, lane_id(), true, L.u, L.prob);
+    update_phase<64>(a, rb, lane_id(), true, L.u, L.prob, nullptr);
     STAMP(a, rb, 1);
-    solve_phase(a, rb, L.prob, L.q);
+    solve_phase(a, rb, L.prob, nullptr, L.q);
     STAMP(a, rb, 6);
 }
 
@@ -1941,11 +2033,15 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_kernel(KernelArgs a) {
     }
     const bool wr = rb < a.batch;  // a padding segment recomputes the last robot, writes nothing
     if (!wr) rb = a.batch - 1;
-    update_phase<UPD_SUB>(a, rb, lane, wr, L.u[seg], L.prob[seg]);
+    update_phase<UPD_SUB>(a, rb, lane, wr, L.u[seg], L.prob[seg], &L.pre[seg]);
+    // work row: [Prob | Presolve]
     const double2* src = reinterpret_cast<const double2*>(&L.prob[seg]);
-    double2* dst = reinterpret_cast<double2*>(a.work + (size_t)rb * PROB_LEN);
-    if (wr)
+    const double2* srp = reinterpret_cast<const double2*>(&L.pre[seg]);
+    double2* dst = reinterpret_cast<double2*>(a.work + (size_t)rb * WORK_LEN);
+    if (wr) {
         for (int k = lane; k < PROB_LEN / 2; k += UPD_SUB) dst[k] = src[k];
+        for (int k = lane; k < PRE_LEN / 2; k += UPD_SUB) dst[PROB_LEN / 2 + k] = srp[k];
+    }
 }
 
 WBC_KERNEL_ATTR void wbc_solve_kernel(KernelArgs a) {
@@ -1956,8 +2052,10 @@ WBC_KERNEL_ATTR void wbc_solve_kernel(KernelArgs a) {
     // per state, read by all of its hypotheses)
     const int row = a.modes ? rb / a.modes : rb;
     double2* dst = reinterpret_cast<double2*>(&L.prob);
-    const double2* src = reinterpret_cast<const double2*>(a.work + (size_t)row * PROB_LEN);
+    const double2* src = reinterpret_cast<const double2*>(a.work + (size_t)row * WORK_LEN);
     for (int k = lane_id(); k < PROB_LEN / 2; k += 64) dst[k] = src[k];
+    // the presolve record stays in HBM / L2: read once, by lanes < 12 and the M unpack
+    const Presolve* pre = reinterpret_cast<const Presolve*>(a.work + (size_t)row * WORK_LEN + PROB_LEN);
     if (a.modes) {  // this hypothesis' contact mask on the unmasked bounds (update_phase)
         const int kap = a.mode_masks[rb - row * a.modes] & 15;
         const int lane = lane_id();
@@ -1969,7 +2067,7 @@ WBC_KERNEL_ATTR void wbc_solve_kernel(KernelArgs a) {
         if (lane == 0) L.prob.kappa = (double)kap;
     }
     wsync();
-    solve_phase(a, rb, L.prob, L.q);
+    solve_phase(a, rb, L.prob, pre, L.q);
 }
 
 __global__ void wbc_reset_kernel(double* hist, const uint8_t* mask, int batch) {

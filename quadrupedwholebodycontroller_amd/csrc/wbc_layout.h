@@ -41,10 +41,22 @@ struct Prob {
     double rsw[12];   // R4/R5 bound: cmd - Js_dot_com v_c - Js_dot_j qdot (cpp:507,515)
     double W[6];      // computeDesiredWrench (cpp:426-445)
     double kappa;     // contact bitmask
-    double flags;     // bit 0: non-finite input / intermediate
+    double flags;     // 1: non-finite input / intermediate, 2: slot Hessian not positive definite
 };
 static_assert(sizeof(Prob) % 16 == 0, "Prob must keep 16-byte alignment");
 constexpr int PROB_LEN = sizeof(Prob) / sizeof(double);
+
+// Slot factorisation formed at the end of the update kernel (presolve in wbc_kernel.hip), stored
+// after the problem in the work row and read by the solve kernel from HBM / L2.
+struct Presolve {
+    double Mi[78];    // M = L^-1 of the slot Hessian H_s = L L^T, lower triangle row-major
+    double xs[12];    // slot part of the unconstrained optimum x0 = -H^-1 g
+    double presolved; // 1: Mi / xs hold the factorisation for this kappa; 0: the solve forms it
+    double pad_;
+};
+static_assert(sizeof(Presolve) % 16 == 0, "Presolve must keep 16-byte alignment");
+constexpr int PRE_LEN = sizeof(Presolve) / sizeof(double);
+constexpr int WORK_LEN = PROB_LEN + PRE_LEN;  // work row: [Prob | Presolve]
 
 // Kernel arguments (one struct, passed by value).
 struct KernelArgs {
@@ -57,7 +69,7 @@ struct KernelArgs {
     const uint8_t* contacts;
     const uint8_t* switching;
     double* hist;       // [B][HIST_LEN]
-    double* work;       // [B][PROB_LEN] (split update/solve)
+    double* work;       // [B][WORK_LEN] (split update/solve): Prob, Presolve
     double* tau;
     double* grf;
     double* x;
