@@ -232,8 +232,8 @@ __device__ __forceinline__ double row0_sum(double v) {
 
 // Segmented forms for the update kernel with several robots per wave (SUB lanes per robot, SUB in
 // {16, 32, 64}): the row sum above, then the segment head's value to every lane of the segment
-// (v_readlane for 64; ds_swizzle bitmask mode, lane & 0x10 or lane & 0 within each 32-lane half,
-// for 16 and 32), so every lane of a robot holds the same bits.
+// (v_readlane for 64; DPP row_newbcast:0 for 16; ds_swizzle bitmask mode, lane & 0 within each
+// 32-lane half, for 32), so every lane of a robot holds the same bits.
 template <int AND>
 __device__ __forceinline__ double swz_head(double v) {
     const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), AND);
@@ -250,7 +250,9 @@ __device__ __forceinline__ double seg_sum(double v) {
         v += dpp_d<0x124>(v);
         v += dpp_d<0x122>(v);
         v += dpp_d<0x121>(v);
-        return swz_head<SUB == 16 ? 0x10 : 0x00>(v);
+        // 16: one robot per DPP row, row_newbcast:0 (a VALU move) instead of an LDS-pipe swizzle
+        if constexpr (SUB == 16) return dpp_d<0x150>(v);
+        else return swz_head<0x00>(v);
     }
 }
 template <int SUB>
