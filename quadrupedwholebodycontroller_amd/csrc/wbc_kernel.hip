@@ -36,11 +36,14 @@ namespace wbc {
 constexpr int NQ = 24;                  // reduced QP variables
 constexpr int C0_LANES = 52;            // max constraints: 7 ns + 24 + 6 (4 - ns) <= 52
 
+// Frames and bodies are read one per lane (lane = body): 25 doubles (50 dwords) apart puts 13
+// consecutive lanes in distinct LDS banks, where 24 doubles (48 dwords) put every 4th lane in the
+// same bank (PMC: ~2 300 bank-conflict cycles per update wave).
 struct Frame {  // world frame of a body after stage A
-    double R[9], o[3], w[3], al[3], ao[3], vo[3];
+    double R[9], o[3], w[3], al[3], ao[3], vo[3], pad;
 };
 struct Body {  // body quantities after stage B
-    double c[3], I[9], F[3], N[3], pad[6];
+    double c[3], I[9], F[3], N[3], pad[7];
 };
 static_assert(sizeof(Frame) == sizeof(Body), "frame / body union");
 
