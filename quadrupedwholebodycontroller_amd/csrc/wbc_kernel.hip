@@ -559,8 +559,8 @@ __device__ bool presolve(const Prob& P, int kap, const wbc_params& pr, int lane,
 // own scratch); lane = lane within the robot's segment; wr = false for a padding segment past the
 // batch (computes a duplicate robot, writes nothing to HBM).
 template <int SUB>
-__device__ void update_phase(const KernelArgs& a, int rb, int lane, bool wr, UpdScratch& s, Prob& P, Presolve* pre) {
-    const wbc_model& md = *a.model;
+__device__ void update_phase(const KernelArgs& a, int rb, int lane, bool wr, UpdScratch& s, Prob& P, Presolve* pre,
+                             const wbc_model& md) {
     const wbc_params& pr = *a.params;
     const int kap = a.contacts[rb];
     const bool switching = a.switching[rb] != 0;
@@ -593,28 +593,37 @@ __device__ void update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
         const bool anybad = wave_any(bad);
         if (lane == 0) { P.flags = anybad ? 1.0 : 0.0; P.kappa = (double)kap; }
     } else {
+        // all loads issued before any is used (addresses clamped to element 90, so every lane
+        // loads); the joint angles' sin / cos come from LDS after the exchange
+        constexpr int NIT = (91 + SUB - 1) / SUB;
+        double v[NIT];
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            const int k = (lane + it * SUB < 91) ? lane + it * SUB : 90;
+            const double* p = (k < 7) ? a.base_pose + (size_t)rb * 7 + k
+                            : (k < 25) ? a.nu + (size_t)rb * 18 + (k - 7)
+                            : (k < 37) ? a.qj + (size_t)rb * 12 + (k - 25)
+                                       : a.ref + (size_t)rb * 54 + (k - 37);
+            v[it] = *p;
+        }
         bool bad = false;
 #pragma unroll
-        for (int it = 0; it < (91 + SUB - 1) / SUB; ++it) {
+        for (int it = 0; it < NIT; ++it) {
             const int k = lane + it * SUB;
             if (k < 91) {
-                const double* p = (k < 7) ? a.base_pose + (size_t)rb * 7 + k
-                                : (k < 25) ? a.nu + (size_t)rb * 18 + (k - 7)
-                                : (k < 37) ? a.qj + (size_t)rb * 12 + (k - 25)
-                                           : a.ref + (size_t)rb * 54 + (k - 37);
-                const double v = *p;
-                bad = bad || !isfinite(v);
-                s.in[k] = v;
+                bad = bad || !isfinite(v[it]);
+                s.in[k] = v[it];
             }
-        }
-        if (lane < 12) {
-            double sn, cs;
-            sincos(a.qj[(size_t)rb * 12 + lane], &sn, &cs);
-            s.sc[lane][0] = sn;
-            s.sc[lane][1] = cs;
         }
         const bool anybad = seg_any<SUB>(bad);
         if (lane == 0) { P.flags = anybad ? 1.0 : 0.0; P.kappa = (double)kap; }
+        lds_sync();
+        if (lane < 12) {
+            double sn, cs;
+            sincos(s.in[25 + lane], &sn, &cs);
+            s.sc[lane][0] = sn;
+            s.sc[lane][1] = cs;
+        }
     }
     lds_sync();
     UST(a, rb, 1);
@@ -1160,16 +1169,16 @@ __device__ void update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
         if (!a.modes) {
             const bool ok = presolve<SUB>(P, kap, pr, lane, s.ps.L, s.ps.ild, s.ps.xs);
             const double (&Mi)[12][12] = *reinterpret_cast<const double(*)[12][12]>(&s.ps.L[0][0]);
-            for (int k = lane; k < 78; k += SUB) {
-                const int i = (int)((sqrt(8.0 * k + 1.0) - 1.0) * 0.5);
-                pre->Mi[k] = Mi[i][k - i * (i + 1) / 2];
+            if (wr) {
+                for (int k = lane; k < 78; k += SUB) {
+                    const int i = (int)((sqrt(8.0 * k + 1.0) - 1.0) * 0.5);
+                    pre->Mi[k] = Mi[i][k - i * (i + 1) / 2];
+                }
+                if (lane < 12) pre->xs[lane] = s.ps.xs[lane];
+                if (lane == 0) pre->presolved = 1.0;
             }
-            if (lane < 12) pre->xs[lane] = s.ps.xs[lane];
-            if (lane == 0) {
-                pre->presolved = 1.0;
-                if (!ok) P.flags += 2.0;
-            }
-        } else if (lane == 0) {
+            if (lane == 0 && !ok) P.flags += 2.0;
+        } else if (lane == 0 && wr) {
             pre->presolved = 0.0;
         }
         lds_sync();
@@ -1734,6 +1743,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, const Pr
         }
     }
     IST_DECL;
+    const int max_wsr = pr.max_wsr;
 
     while (!done) {
         // compiler barrier: LDS reads of the problem (build_normal / to_column on the rare drop
@@ -1783,7 +1793,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, const Pr
                 pstar = idx;
                 up = 0.0;
             }
-            if (++iters > pr.max_wsr) { status = WBC_QP_MAX_ITER; iters = pr.max_wsr; break; }
+            if (++iters > max_wsr) { status = WBC_QP_MAX_ITER; iters = max_wsr; break; }
             col = pstar;
             pos = q;
         }
@@ -2006,8 +2016,8 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, const Pr
 #endif
 constexpr int UPD_SUB = WBC_UPDATE_SUB, UPD_RPW = 64 / UPD_SUB;
 struct UpdLds {
+    wbc_model model;  // staged once per wave: the kinematic chain reads it at lane-varying addresses
     Prob prob[UPD_RPW];
-    Presolve pre[UPD_RPW];
     UpdScratch u[UPD_RPW];
 };
 struct SolveLds {
@@ -2020,7 +2030,7 @@ WBC_KERNEL_ATTR void wbc_step_kernel(KernelArgs a) {
     const int rb = xcd_robot();
     if (rb >= a.batch) return;
     STAMP(a, rb, 0);
-    update_phase<64>(a, rb, lane_id(), true, L.u, L.prob, nullptr);
+    update_phase<64>(a, rb, lane_id(), true, L.u, L.prob, nullptr, *a.model);
     STAMP(a, rb, 1);
     solve_phase(a, rb, L.prob, nullptr, L.q);
     STAMP(a, rb, 6);
@@ -2038,14 +2048,19 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_kernel(KernelArgs a) {
     }
     const bool wr = rb < a.batch;  // a padding segment recomputes the last robot, writes nothing
     if (!wr) rb = a.batch - 1;
-    update_phase<UPD_SUB>(a, rb, lane, wr, L.u[seg], L.prob[seg], &L.pre[seg]);
-    // work row: [Prob | Presolve]
+    {
+        const double* gm = reinterpret_cast<const double*>(a.model);
+        double* lm = reinterpret_cast<double*>(&L.model);
+        for (int k = (int)threadIdx.x; k < (int)(sizeof(wbc_model) / 8); k += 64) lm[k] = gm[k];
+    }
+    lds_sync();
+    // work row: [Prob | Presolve]; the Presolve record is stored by update_phase itself
+    Presolve* pre = reinterpret_cast<Presolve*>(a.work + (size_t)rb * WORK_LEN + PROB_LEN);
+    update_phase<UPD_SUB>(a, rb, lane, wr, L.u[seg], L.prob[seg], pre, L.model);
     const double2* src = reinterpret_cast<const double2*>(&L.prob[seg]);
-    const double2* srp = reinterpret_cast<const double2*>(&L.pre[seg]);
     double2* dst = reinterpret_cast<double2*>(a.work + (size_t)rb * WORK_LEN);
     if (wr) {
         for (int k = lane; k < PROB_LEN / 2; k += UPD_SUB) dst[k] = src[k];
-        for (int k = lane; k < PRE_LEN / 2; k += UPD_SUB) dst[PROB_LEN / 2 + k] = srp[k];
     }
 }
 
