@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Benchmark: batched ANYmal WBC QP solves/s on MI355X (BASELINE.json metric).
 
-One step = one wbc_step over the rank's batch (dynamics + centroidal assembly + QP + torques,
-one fused HIP kernel), plus for N > 1 the RCCL all-gather of the torque block.  Inputs are
+One step = one wbc_step over the rank's batch (dynamics + centroidal assembly + QP + torques:
+the update kernel then the solve kernel, the build's default form), plus for N > 1 the RCCL
+all-gather of the torque block.  Inputs are
 resident in HBM before the timed region.  Default workload: configs[1] of BASELINE.json,
 B = 4096 four-contact stance states, cold solves, per GPU (weak scaling).
 

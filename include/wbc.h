@@ -179,8 +179,9 @@ int32_t wbc_reset(wbc_engine* h, const uint8_t* mask);
 int32_t wbc_update(wbc_engine* h, uint32_t flags);
 /* solveQP() + computeJointTorques() on the problem assembled by the last wbc_update. */
 int32_t wbc_solve(wbc_engine* h, uint32_t flags);
-/* update + solve + torques for one control cycle: one fused kernel (the problem stays in LDS), or
- * under WBC_SPLIT the update kernel then the solve kernel (the problem passes through HBM). */
+/* update + solve + torques for one control cycle: by default the update kernel then the solve
+ * kernel (the problem passes through HBM; WBC_SPLIT forces this form), or under WBC_FUSED one fused
+ * kernel (the problem stays in LDS). */
 int32_t wbc_step(wbc_engine* h, uint32_t flags);
 int32_t wbc_synchronize(wbc_engine* h);
 

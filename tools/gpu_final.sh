@@ -11,6 +11,7 @@ step pytest 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-m
 step smoke 120 python -c "import __graft_entry__ as g; g.smoke()"
 step pmc 600 env TAG=$TAG bash tools/pmc.sh
 cp gpurun_out/pmc_$TAG/pmc_summary.json $O/pmc_stance_cold_b4096.json
+cp $O/pmc_stance_cold_b4096.json profiles/r01/pmc_stance_cold_b4096.json  # read by bench.py below
 step bench 300 python bench.py --steps 50 --warmup 5
 step bench_extra 300 python bench.py --steps 20 --warmup 3 --extra --breakdown --no-cpu-baseline
 step prof 300 rocprofv3 --kernel-trace --stats -d $O/prof -o prof --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline
