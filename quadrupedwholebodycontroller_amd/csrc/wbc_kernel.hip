@@ -1444,7 +1444,16 @@ __device__ void active_set_point(const QpScratch& s, int q, int act, double sp0,
     sp = sp0 + ((s4[0] + s4[1]) + (s4[2] + s4[3]));
 }
 
-__device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, const Presolve* pre, QpScratch& s) {
+// The Presolve record in registers: packed entry `lane` in v0 and 64 + lane in v1, loaded at the
+// solve kernel's start so that its HBM round trip overlaps the problem copy
+struct PreRegs {
+    double v0, v1;
+};
+constexpr int PRE_FLAG = 90;  // packed index of Presolve::presolved
+static_assert(offsetof(Presolve, presolved) == PRE_FLAG * sizeof(double), "PRE_FLAG");
+static_assert(offsetof(Presolve, xs) == 78 * sizeof(double), "Presolve packing");
+
+__device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, const PreRegs* pf, QpScratch& s) {
     const wbc_params& pr = *a.params;
     const int lane = lane_id();
     const int kap = (int)P.kappa;
@@ -1466,12 +1475,23 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, const Pr
 #pragma unroll
         for (int j = 0; j < 12; j += 2) *reinterpret_cast<double2*>(&s.G[lane][j]) = make_double2(grow[j], grow[j + 1]);
     }
-    if (pre && pre->presolved != 0.0) {
+    if (pf && bcast(pf->v1, PRE_FLAG - 64) != 0.0) {
+        // unpack: packed p < 78 is M(i, j), p = i (i + 1) / 2 + j; 78..89 are xs
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int p = lane + 64 * h;
+            const double v = h ? pf->v1 : pf->v0;
+            if (p < 78) {
+                const int i = (int)((sqrt(8.0 * p + 1.0) - 1.0) * 0.5);
+                s.Mi()[i][p - i * (i + 1) / 2] = v;
+            } else if (p < 90) {
+                s.xs[p - 78] = v;
+            }
+        }
         for (int k = lane; k < 144; k += 64) {
             const int i = k / 12, j = k % 12;
-            s.Mi()[i][j] = (j <= i) ? pre->Mi[i * (i + 1) / 2 + j] : 0.0;
+            if (j > i) s.Mi()[i][j] = 0.0;
         }
-        if (lane < 12) s.xs[lane] = pre->xs[lane];
     } else if (!presolve<64>(P, kap, pr, lane, s.L, s.ild, s.xs) && status == WBC_QP_OK) {
         status = WBC_QP_NUMERIC;
     }
@@ -2071,11 +2091,14 @@ WBC_KERNEL_ATTR void wbc_solve_kernel(KernelArgs a) {
     // mode hypotheses: QP rb is hypothesis rb % modes of state rb / modes (one assembled problem
     // per state, read by all of its hypotheses)
     const int row = a.modes ? rb / a.modes : rb;
+    // the Presolve record goes to registers, its loads issued before the problem copy's
+    const double* prow = a.work + (size_t)row * WORK_LEN + PROB_LEN;
+    PreRegs pf;
+    pf.v0 = prow[lane_id()];
+    pf.v1 = prow[lane_id() < PRE_LEN - 64 ? 64 + lane_id() : PRE_LEN - 1];
     double2* dst = reinterpret_cast<double2*>(&L.prob);
     const double2* src = reinterpret_cast<const double2*>(a.work + (size_t)row * WORK_LEN);
     for (int k = lane_id(); k < PROB_LEN / 2; k += 64) dst[k] = src[k];
-    // the presolve record stays in HBM / L2: read once, by lanes < 12 and the M unpack
-    const Presolve* pre = reinterpret_cast<const Presolve*>(a.work + (size_t)row * WORK_LEN + PROB_LEN);
     if (a.modes) {  // this hypothesis' contact mask on the unmasked bounds (update_phase)
         const int kap = a.mode_masks[rb - row * a.modes] & 15;
         const int lane = lane_id();
@@ -2087,7 +2110,7 @@ WBC_KERNEL_ATTR void wbc_solve_kernel(KernelArgs a) {
         if (lane == 0) L.prob.kappa = (double)kap;
     }
     wsync();
-    solve_phase(a, rb, L.prob, pre, L.q);
+    solve_phase(a, rb, L.prob, &pf, L.q);
 }
 
 __global__ void wbc_reset_kernel(double* hist, const uint8_t* mask, int batch) {
