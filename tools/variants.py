@@ -42,6 +42,10 @@ o = e.outputs()
 res["modes16_b16384"] = dict(ms=ms, solves_per_s=S * 16 / ms * 1e3, status=[int(x) for x in __import__("numpy").bincount(o["status"], minlength=4)],
                              tau_sum=float(abs(o["tau"]).sum()))
 e.close()
+import bench  # configs[2]: stateful trot (history + hotstart), 100 cycles
+r = bench.bench_trot(torch, st, 0, STATELESS, T=100)
+res["trot_b4096"] = dict(ms=r["ms_per_step"], solves_per_s=r["solves_per_s"], status=r["status_counts_last"],
+                         mean_iters=r["mean_iters_last"])
 print(json.dumps(res))
 ''' % ROOT
 steps = sys.argv[1] if len(sys.argv) > 1 else "30"
