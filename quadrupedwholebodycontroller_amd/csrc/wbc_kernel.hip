@@ -1183,6 +1183,7 @@ __device__ void update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
         }
         lds_sync();
     }
+    UST(a, rb, 11);  // slot 19; slots 20.. belong to the solve (EST)
 }
 
 // ---------------------------------------------------------------------------------------

@@ -1,0 +1,27 @@
+"""Cycles per stage of the split-mode update kernel (four robots per wave), from the WBC_ISTAMPS
+build.  The stamps are written by lane 0 of each wave, so only robots rb % 4 == 0 carry them.
+Usage (GPU box): WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_istamps.so python tools/ustamps.py [config] [B]"""
+import json, os, sys
+import numpy as np
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from quadrupedwholebodycontroller_amd import STATELESS, Engine, workloads
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "stance_cold"
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+inp = getattr(workloads, cfg)(B, seed=1 if cfg == "stance_cold" else 3)
+e = Engine(B)
+e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
+e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
+for _ in range(3):
+    e.step(STATELESS)  # default split form: update kernel, then solve kernel
+e.synchronize()
+u = e.debug()[0::4, 8:20]
+un = ["inputs+sincos", "stage A (leg chains)", "stage B (bodies)", "Jf + CoM sums", "Ic sum+inv", "stage C (joints)",
+      "hb sum, y, zeta, lane0", "Jbar/Mbar/bbar", "Tdot_inv", "bounds, wrench, history",
+      "slot Cholesky (presolve) + store"]
+du = np.diff(u, axis=1)
+ok = (u > 0).all(1)
+res = {n: float(np.median(du[ok, i])) for i, n in enumerate(un)}
+res["total (stamps 0..11)"] = float(np.median(u[ok, -1] - u[ok, 0]))
+res["robots sampled"] = int(ok.sum())
+print(json.dumps(dict(config=cfg, batch=B, split_update_cycles=res), indent=1))
