@@ -29,13 +29,20 @@ BYTES_COLD = 929          # 729 B in + 200 B out per cold solve
 BYTES_IN, BYTES_OUT = 729, 200  # per state read / per QP written (mode hypotheses share the state read)
 
 CONFIGS = {
-    "stance_cold_b4096": dict(gen="stance_cold", batch=4096, seed=1,
+    "stance_cold_b4096": dict(gen="stance_cold", batch=4096, seed=1, scaling="weak",
                               desc="BASELINE configs[1]: B=4096 4-contact stance QPs, fp64, cold start"),
-    "rl_random_b8192": dict(gen="rl_random", batch=8192, seed=3,
+    "rl_random_b8192": dict(gen="rl_random", batch=8192, seed=3, scaling="weak",
                             desc="BASELINE configs[3] per-GPU shard: randomized q/qd, 16 contact masks, cold"),
-    "modes16_b16384": dict(gen="modes16", batch=16384, seed=4, modes=16,
+    "modes16_b16384": dict(gen="modes16", batch=16384, seed=4, modes=16, scaling="weak",
                            desc="BASELINE configs[4] per-GPU shard: 1024 states x all 16 contact masks, cold; "
                                 "wbc_step_modes (dynamics + assembly once per state, 16 QPs per state)"),
+    # the two multi-GPU configurations at their global sizes (strong scaling: total work fixed)
+    "rl_random_b65536": dict(gen="rl_random", batch=65536, seed=3, scaling="strong",
+                             desc="BASELINE configs[3]: global B=65536 randomized q/qd (16 contact masks, cold), "
+                                  "contiguous robot shards per GPU"),
+    "modes16_x8192": dict(gen="modes16", batch=131072, seed=4, modes=16, scaling="strong",
+                          desc="BASELINE configs[4]: 8192 states x 16 contact masks = 131072 QPs, sharded by state "
+                               "(a state's 16 hypotheses on one GPU)"),
 }
 
 
@@ -181,65 +188,147 @@ def bench_trot(torch, stream, device, STATELESS, B=4096, T=400, seed=2):
                 desc="BASELINE configs[2]: trot, alternating 2-contact modes, stateful history, inputs staged in HBM")
 
 
+def _self_launch(n):
+    """`--gpus N` without a torch.distributed environment: run this same command as N ranks under
+    torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1) as a child process and
+    return its exit code.  Nothing here has touched the GPU yet."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd, env=env).returncode
+
+
+def shard_inputs(cfg, scaling, world, rank):
+    """Inputs of this rank: (B_rank QPs, S_rank input rows, inputs, modes or None, global QPs).
+    weak: a full per-GPU batch, seed + 1000 rank; strong: the rank's contiguous shard of the
+    global batch (mode hypotheses shard by state, so a state's 16 QPs stay on one rank)."""
+    from quadrupedwholebodycontroller_amd import workloads
+    from quadrupedwholebodycontroller_amd.sharding import shard_bounds
+
+    K = cfg.get("modes", 0)
+    B = cfg["batch"]
+    S = B // K if K else B
+    if scaling == "weak":
+        seed = cfg["seed"] + 1000 * rank
+        lo, hi, S_tot = 0, S, S * world
+    else:
+        seed = cfg["seed"]
+        lo, hi = shard_bounds(S, world, rank)
+        S_tot = S
+    if K:
+        inp, modes = workloads.mode_states(S if scaling == "strong" else S, seed)
+    else:
+        inp, modes = getattr(workloads, cfg["gen"])(S, seed=seed), None
+    if scaling == "strong":
+        inp = {k: np.ascontiguousarray(v[lo:hi]) for k, v in inp.items()}
+    S_rank = hi - lo
+    return S_rank * (K or 1), S_rank, inp, modes, S_tot * (K or 1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="stance_cold_b4096", choices=sorted(CONFIGS))
-    ap.add_argument("--batch", type=int, default=0, help="override per-GPU batch")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default=None,
+                    help="weak: the config's batch per GPU; strong: the config's batch in total, sharded "
+                         "(default: the config's own)")
+    ap.add_argument("--batch", type=int, default=0, help="override the config's batch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--extra", action="store_true", help="also time the other configs (reported under 'extra')")
     ap.add_argument("--breakdown", action="store_true", help="also time the update and solve kernels separately")
     args = ap.parse_args()
 
-    import torch
-
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_self_launch(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+        sys.exit(2)
+
+    import torch
+
+    torch.cuda.set_device(local_rank)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    else:
-        torch.cuda.set_device(local_rank)
 
-    from quadrupedwholebodycontroller_amd import FUSED, NO_X, STATELESS, Engine, workloads
+    from quadrupedwholebodycontroller_amd import FUSED, NO_X, STATELESS, Engine
+    from quadrupedwholebodycontroller_amd.sharding import (StepOutputs, gather_step_outputs, shard_capacity,
+                                                           unpack_gathered)
 
     STEP_FLAGS = STATELESS | NO_X  # cold solves; outputs tau, grf, status, iters (the published ones)
 
-    cfg = CONFIGS[args.config]
-    B = args.batch or cfg["batch"]
+    cfg = dict(CONFIGS[args.config])
+    if args.batch:
+        cfg["batch"] = args.batch
+    scaling = args.scaling or cfg.get("scaling", "weak")
     K = cfg.get("modes", 0)
-    S = B // K if K else B  # input rows (states)
+    B, S, inp, modes, B_total = shard_inputs(cfg, scaling, world, rank)
 
-    # a dedicated (non-null) stream: the engine launches on it, the RCCL all-gather is ordered on it,
-    # and the HIP events below time it (the legacy null stream would be handle 0 = "engine default")
+    # a dedicated (non-null) stream: the engine launches on it and the HIP events below time it (the
+    # legacy null stream would be handle 0 = "engine default"); the all-gather runs on `comm`
     stream = torch.cuda.Stream()
+    comm = torch.cuda.Stream() if world > 1 else None
     torch.cuda.set_stream(stream)
-    e, step, inp = make_engine(cfg, B, cfg["seed"] + 1000 * rank, local_rank, stream)
-    tau_local = torch.zeros(B * 12, dtype=torch.float64, device="cuda")
-    e.bind_device_outputs(tau=tau_local.data_ptr())
-    tau_all = torch.zeros(world * B * 12, dtype=torch.float64, device="cuda") if world > 1 else None
+    e = Engine(B, device=local_rank)
+    e.set_stream(stream.cuda_stream)
+    if K:
+        e.set_modes(modes)
+    e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
+    e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
+    step = e.step_modes if K else e.step
 
-    def one_step():
+    # Step outputs go straight into packed blocks (tau | status | iters) that the step's one
+    # collective gathers (sharding.gather_step_outputs).  Two blocks alternate, so that the gather of
+    # step k (on `comm`) overlaps step k + 1; step k + 2 waits for it before overwriting the block.
+    cap = shard_capacity(B_total // (K or 1), world) * (K or 1) if scaling == "strong" else B
+    blocks = [StepOutputs(cap, device="cuda") for _ in range(2)]
+    gathered = [torch.empty(world * cap * 13, dtype=torch.float64, device="cuda") for _ in range(2)] \
+        if world > 1 else None
+    ev_step = [torch.cuda.Event() for _ in range(2)]
+    ev_gath = [torch.cuda.Event() for _ in range(2)]
+    used = [False, False]
+
+    def bind(slot):
+        b = blocks[slot]
+        e.bind_device_outputs(tau=b.tau.data_ptr(), status=b.status.data_ptr(), iters=b.iters.data_ptr())
+
+    def one_step(k):
+        slot = k & 1
+        if world > 1 and used[slot]:
+            stream.wait_event(ev_gath[slot])  # the gather of step k - 2 has read this block
+        bind(slot)
         step(STEP_FLAGS)
         if world > 1:
-            dist.all_gather_into_tensor(tau_all, tau_local)
+            ev_step[slot].record(stream)
+            with torch.cuda.stream(comm):
+                comm.wait_event(ev_step[slot])
+                gather_step_outputs(blocks[slot], world, out=gathered[slot])
+                ev_gath[slot].record(comm)
+            used[slot] = True
 
-    for _ in range(args.warmup):
-        one_step()
+    for k in range(args.warmup):
+        one_step(k)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        one_step()
+    for k in range(args.steps):
+        one_step(args.warmup + k)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -249,10 +338,20 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+    last = (args.warmup + args.steps - 1) & 1
+    # whole-batch outputs of the last timed step, as every rank holds them after the gather
+    if world > 1:
+        g_tau, g_status, g_iters = unpack_gathered(gathered[last], B * world if scaling == "weak" else B_total,
+                                                   world, unit=K or 1)
+    else:
+        g_tau = blocks[last].tau[: B * 12].cpu().numpy().reshape(B, 12)
+        g_status = blocks[last].status[:B].cpu().numpy()
+        g_iters = blocks[last].iters[:B].cpu().numpy()
+    bind(0)
 
     # Kernel duration for the roofline: HIP events on the launch stream around K back-to-back
-    # launches of the step kernel (the engine's only kernel per step; this includes the few-us
-    # dispatch gap between launches, which rocprofv3's per-dispatch average in profiles/ excludes).
+    # launches (this includes the few-us dispatch gap between launches, which rocprofv3's
+    # per-dispatch average in profiles/ excludes).
     def timed(fn):
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record(stream)
@@ -300,7 +399,7 @@ def main():
     if args.extra and rank == 0:
         extra["trot_stateful_b4096"] = bench_trot(torch, stream, local_rank, STATELESS)
         for name, c2 in CONFIGS.items():
-            if name == args.config:
+            if name == args.config or c2.get("scaling") == "strong":
                 continue
             B2 = c2["batch"]
             e2, step2, _ = make_engine(c2, B2, c2["seed"], local_rank, stream)
@@ -314,7 +413,7 @@ def main():
             e2.close()
 
     traffic, traffic_src = committed_traffic(args.config, B)
-    total = B * world * args.steps
+    total = (B * world if scaling == "weak" else B_total) * args.steps
     value = total / elapsed
     result = {
         "metric": "WBC QP solves/sec (ANYmal 18-DoF, 4-contact) at 1/2/4/8 GPUs; % HBM roofline",
@@ -325,29 +424,33 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (SURVEY.md 8d generators, numpy PCG64 seed %d + 1000*rank)" % cfg["seed"],
+        "data": "synthetic (SURVEY.md 8d generators, numpy PCG64 seed %d%s)"
+                % (cfg["seed"], " + 1000*rank" if scaling == "weak" else ", global batch sharded by rank"),
         "config": {"workload": args.config, "description": cfg["desc"], "batch_per_gpu": B,
-                   "global_batch": B * world, "parallelism": f"dp{world} (robot shards) + RCCL all-gather of tau"
-                   if world > 1 else "dp1"},
-        "roofline": {"bound": "mfma", "achieved": tf_dom, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                   "global_batch": B * world if scaling == "weak" else B_total,
+                   "parallelism": f"dp{world}" + (" (robot shards; RCCL all-gather of tau|status|iters per step, "
+                                                  "overlapped with the next step)" if world > 1 else "")},
+        "roofline": {"bound": "fp64_valu", "achieved": tf_dom, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": tf_dom / FP64_PEAK_TFLOPS, "traffic": traffic.get(dom),
                      "traffic_source": traffic_src, "kernel": dom, "kernel_ms": dom_ms,
                      "kernels_ms": kernels, "step_kernels_ms": step_ms,
-                     "note": "dominant kernel; fp64 compute roof (gfx950 fp64 vector = matrix peak); algorithmic "
-                             "flops of SURVEY 8(d) owned by this kernel (F_fact + F_tau + k F_iter, k = iters[] per "
-                             "robot); latency/issue-bound small dense linear algebra"},
+                     "note": "dominant kernel; fp64 VALU roof (no MFMA on this path; gfx950 fp64 vector peak); "
+                             "algorithmic flops of SURVEY 8(d) owned by this kernel (F_fact + F_tau + k F_iter, "
+                             "k = iters[] per robot); latency/issue-bound small dense linear algebra"},
         "roofline_hbm": {"bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": hbm_gbs / HBM_PEAK_GBS, "bytes_per_solve": bytes_step / B,
                          "traffic": (traffic.get("wbc_update_kernel", 0) + traffic.get("wbc_solve_kernel", 0))
                          if traffic else None,
                          "note": "algorithmic bytes over the step (both kernels): 729 B read per state + 200 B "
                                  "written per QP (929 B/solve one QP per state); traffic = PMC bytes per step "
-                                 "(both kernels, incl. the 2.9 KB/state problem hand-off)"},
+                                 "(both kernels, incl. the problem hand-off between them)"},
         "qp_status_counts": np.bincount(status, minlength=4).tolist(),
         "mean_iters": float(iters.mean()),
+        "gathered": {"robots": int(len(g_status)), "status_counts": np.bincount(g_status, minlength=4).tolist(),
+                     "mean_iters": float(np.mean(g_iters)), "tau_abs_sum": float(np.abs(g_tau).sum())},
     }
     if extra:
         result["extra"] = extra
@@ -358,6 +461,8 @@ def main():
         import multiprocessing
 
         result["cpu_baseline"]["host"] = dict(nproc=multiprocessing.cpu_count(), model=_cpu_model())
+    elif world > 1:
+        result["cpu_baseline_note"] = "timed at N=1 only (rank 0), per the bench contract"
     e.close()
     if world > 1:
         dist.destroy_process_group()

@@ -281,9 +281,19 @@ void wbc_ref_kindyn(const wbc_model* md, const double* pose, const double* nu, c
 
 /* ------------------------------------------------------------------ Goldfarb-Idnani (dense) */
 /* min 1/2 x'Hx + g'x  s.t. CE x = ce (me rows), CI x >= ci (mi rows); n <= NV. */
+/* Warm start (qpOASES SQProblem::hotstart from the previous working set, cpp:523-535): the nwarm
+ * inequality ids in warm[] (the active set the previous solve ended with, same contact mask) are
+ * added after the equalities without steps; the point where every active row holds with equality
+ * then gives the multipliers in closed form (R'v = -s_A(x0), u = R^-1 v, x = x0 + J1 v).  A
+ * dependent warm row or a multiplier below -1e-10 rejects the warm set and the solve continues
+ * from the equality-constrained point, as a cold solve.  Re-adds are not counted in iters (only
+ * working-set changes of the loop are).  On return act_out[0..*nact_out) holds the active
+ * inequality ids (for the next hotstart). */
 static int gi_solve(int n, const double* H, const double* g, int me, const double* CE, const double* ce, int mi,
-                    const double* CI, const double* ci, int max_iter, double* x, int* iters_out) {
-    double L[NV * NV], J[NV * NV], R[NV * NV], u[NV], d[NV], z[NV], r[NV], ni[2 * NC];
+                    const double* CI, const double* ci, int max_iter, const int* warm, int nwarm, double* x,
+                    int* iters_out, int* act_out, int* nact_out) {
+    double L[NV * NV], J[NV * NV], R[NV * NV], u[NV], d[NV], z[NV], r[NV], ni[2 * NC], x0[NV];
+    if (nact_out) *nact_out = 0;
     int act[NV]; /* >= 0: inequality id ; < 0: equality -(id+1) */
     int q = 0, iters = 0;
     const double eps = 1e-14;
@@ -325,6 +335,7 @@ static int gi_solve(int n, const double* H, const double* g, int me, const doubl
             x[i] = -s;
         }
     }
+    memcpy(x0, x, sizeof(double) * n);
     memset(R, 0, sizeof R);
     for (int i = 0; i < mi; ++i) {
         double s = 0.0;
@@ -395,6 +406,76 @@ static int gi_solve(int n, const double* H, const double* g, int me, const doubl
         if (!ok) return WBC_REF_NUMERIC;
     }
     const int n_eq = q;
+    for (int w = 0; w < nwarm; ++w)
+        if (warm[w] < 0 || warm[w] >= mi) nwarm = 0;
+    if (nwarm > 0 && n_eq + nwarm <= n) {
+        static __thread double Js[NV * NV], Rs[NV * NV];
+        double xs[NV], us[NV];
+        int acts[NV];
+        memcpy(Js, J, sizeof J);
+        memcpy(Rs, R, sizeof R);
+        memcpy(xs, x, sizeof xs);
+        memcpy(us, u, sizeof us);
+        memcpy(acts, act, sizeof acts);
+        int ok = 1;
+        for (int w = 0; w < nwarm && ok; ++w) {
+            const double* np_ = CI + warm[w] * n;
+            for (int i = 0; i < n; ++i) {
+                double s_ = 0.0;
+                for (int k = 0; k < n; ++k) s_ += J[k * NV + i] * np_[k];
+                d[i] = s_;
+            }
+            act[q] = warm[w];
+            ADD_CONSTRAINT(ok);
+        }
+        if (ok) {
+            /* R' v = -s_A(x0) (forward), u = R^-1 v (backward), x = x0 + J[:, 0:q] v */
+            double v[NV], sa[NV];
+            for (int k = 0; k < q; ++k) {
+                const double* row = act[k] < 0 ? CE + (-act[k] - 1) * n : CI + act[k] * n;
+                double s_ = act[k] < 0 ? -ce[-act[k] - 1] : -ci[act[k]];
+                for (int i = 0; i < n; ++i) s_ += row[i] * x0[i];
+                sa[k] = s_;
+            }
+            for (int k = 0; k < q; ++k) {
+                double s_ = -sa[k];
+                for (int i = 0; i < k; ++i) s_ -= R[i * NV + k] * v[i];
+                v[k] = s_ / R[k * NV + k];
+            }
+            for (int k = q - 1; k >= 0; --k) {
+                double s_ = v[k];
+                for (int i = k + 1; i < q; ++i) s_ -= R[k * NV + i] * u[i];
+                u[k] = s_ / R[k * NV + k];
+            }
+            for (int k = n_eq; k < q; ++k)
+                if (u[k] < -1e-10) ok = 0;
+            if (ok) {
+                for (int i = 0; i < n; ++i) {
+                    double s_ = x0[i];
+                    for (int k = 0; k < q; ++k) s_ += J[i * NV + k] * v[k];
+                    x[i] = s_;
+                }
+                for (int k = n_eq; k < q; ++k)
+                    if (u[k] < 0.0) u[k] = 0.0;
+            }
+        }
+        if (!ok) { /* reject: back to the equality-constrained point */
+            memcpy(J, Js, sizeof J);
+            memcpy(R, Rs, sizeof R);
+            memcpy(x, xs, sizeof xs);
+            memcpy(u, us, sizeof us);
+            memcpy(act, acts, sizeof acts);
+            q = n_eq;
+        }
+    }
+#define GI_RETURN(st_)                                                                 \
+    do {                                                                               \
+        if (act_out && nact_out) {                                                     \
+            for (int k_ = n_eq; k_ < q; ++k_) act_out[k_ - n_eq] = act[k_];           \
+            *nact_out = q - n_eq;                                                      \
+        }                                                                              \
+        return (st_);                                                                  \
+    } while (0)
     for (;;) {
         /* most violated inactive inequality (scaled) */
         int p = -1;
@@ -409,7 +490,7 @@ static int gi_solve(int n, const double* H, const double* g, int me, const doubl
             double tol = 1e-10 * (fabs(ci[i]) > 1.0 ? fabs(ci[i]) : 1.0);
             if (s < -tol && s / ni[i] < best) { best = s / ni[i]; p = i; }
         }
-        if (p < 0) { *iters_out = iters; return WBC_REF_OK; }
+        if (p < 0) { *iters_out = iters; GI_RETURN(WBC_REF_OK); }
         const double* np_ = CI + p * n;
         double sp = -ci[p];
         for (int k = 0; k < n; ++k) sp += np_[k] * x[k];
@@ -466,12 +547,13 @@ static int gi_solve(int n, const double* H, const double* g, int me, const doubl
     }
 #undef COMPUTE_DZR
 #undef ADD_CONSTRAINT
+#undef GI_RETURN
 }
 
 /* qpOASES general constraints lbA <= A x <= ubA -> (CE, CI); identically-zero rows (quirk A.12) are
  * dropped when feasible for x, flagged infeasible otherwise; two-sided rows are split. */
 static int solve_qp(const double* H, const double* g, const double* A, const double* lb, const double* ub, int max_iter,
-                    double* x, int* iters) {
+                    const int* warm, int nwarm, double* x, int* iters, int* act_out, int* nact_out) {
     static const int n = NV;
     double CE[NC * NV], ce[NC], CI[2 * NC * NV], ci[2 * NC];
     int me = 0, mi = 0;
@@ -504,7 +586,7 @@ static int solve_qp(const double* H, const double* g, const double* A, const dou
             ci[mi++] = -ub[i];
         }
     }
-    return gi_solve(n, H, g, me, CE, ce, mi, CI, ci, max_iter, x, iters);
+    return gi_solve(n, H, g, me, CE, ce, mi, CI, ci, max_iter, warm, nwarm, x, iters, act_out, nact_out);
 }
 
 /* ------------------------------------------------------------------ controller */
@@ -685,11 +767,18 @@ int wbc_ref_step(const wbc_model* md, const wbc_params* pr, wbc_ref_state* st, c
             ub[34 + i] = pr->max_torque - bbar[6 + i];
         }
     }
-    int it = 0;
-    int status = solve_qp(H, g, A, lb, ub, pr->max_wsr, x, &it);
+    int it = 0, nact = 0, act[NV];
+    /* init on the first cycle, hotstart from the previous working set afterwards (cpp:523-531);
+     * the working set only carries over under the same contact mask (the constraint rows differ
+     * otherwise) */
+    const int warm = st->first && !st->cold_qp && st->ws_n > 0 && st->ws_kap == contacts;
+    int status = solve_qp(H, g, A, lb, ub, pr->max_wsr, warm ? st->ws : NULL, warm ? st->ws_n : 0, x, &it, act, &nact);
     *iters = it;
     st->contacts = contacts;
     st->first = 1;
+    st->ws_kap = contacts;
+    st->ws_n = (status == WBC_REF_OK) ? nact : 0;
+    for (int k = 0; k < st->ws_n; ++k) st->ws[k] = act[k];
     if (status != WBC_REF_OK) {
         memset(x, 0, sizeof(double) * NV);
         memset(tau, 0, sizeof(double) * NJ);

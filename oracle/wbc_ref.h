@@ -19,6 +19,8 @@ typedef struct {
 typedef struct {
     double old_T[18 * 18], old_Jc[12 * 18], old_Js[12 * 18], Tdot_inv[18 * 18], e_int[6];
     int contacts, first;
+    int ws_n, ws_kap, cold_qp; /* working set of the last solve (hotstart, cpp:531); cold_qp: always init */
+    int ws[42];
 } wbc_ref_state;
 
 typedef struct {

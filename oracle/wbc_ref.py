@@ -28,7 +28,8 @@ class KinDyn(C.Structure):
 class State(C.Structure):
     _fields_ = [("old_T", C.c_double * 324), ("old_Jc", C.c_double * 216), ("old_Js", C.c_double * 216),
                 ("Tdot_inv", C.c_double * 324), ("e_int", C.c_double * 6), ("contacts", C.c_int),
-                ("first", C.c_int)]
+                ("first", C.c_int), ("ws_n", C.c_int), ("ws_kap", C.c_int), ("cold_qp", C.c_int),
+                ("ws", C.c_int * 42)]
 
 
 class Debug(C.Structure):
@@ -115,9 +116,16 @@ def _p(a):
     return a.ctypes.data_as(C.c_void_p)
 
 
-def run_batch(inp):
-    """Cold batch (every robot from setInitialState with the given switching flags)."""
+def run_batch(inp, **overrides):
+    """Cold batch (every robot from setInitialState with the given switching flags).  Keyword
+    arguments override wbc_params fields (e.g. max_torque=6.0, max_wsr=2)."""
     m, p = model_params()
+    if overrides:
+        p2 = type(p)()
+        C.pointer(p2)[0] = p
+        for k, v in overrides.items():
+            setattr(p2, k, v)
+        p = p2
     B = inp["base_pose"].shape[0]
     f = lambda k, dt=np.float64: np.ascontiguousarray(inp[k], dt)
     pose, nu, qj, ref = f("base_pose"), f("nu"), f("qj"), f("ref")
@@ -132,12 +140,22 @@ def run_batch(inp):
 class Robot:
     """Stateful single robot (the reference object across cycles)."""
 
-    def __init__(self):
+    def __init__(self, hotstart=True, **overrides):
+        """hotstart: qpOASES init on the first cycle, then hotstart from the previous working set
+        (cpp:523-531); False: every solve cold (the engine's WBC_COLD).  overrides: wbc_params fields."""
         self.st = State()
         lib().wbc_ref_state_init(C.byref(self.st))
+        self.st.cold_qp = 0 if hotstart else 1
+        self.overrides = overrides
 
     def step(self, pose, nu, qj, ref, contacts, switching, debug=False):
         m, p = model_params()
+        if self.overrides:
+            p2 = type(p)()
+            C.pointer(p2)[0] = p
+            for k, v in self.overrides.items():
+                setattr(p2, k, v)
+            p = p2
         tau, grf, x = np.zeros(12), np.zeros(12), np.zeros(42)
         it = C.c_int()
         dbg = Debug() if debug else None

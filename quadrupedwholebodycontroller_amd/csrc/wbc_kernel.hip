@@ -1227,7 +1227,7 @@ __device__ __forceinline__ int nth_leg(int kap, int idx, int want) {
 //   R3  torque limits     +-(Mbar_j qdd - Jc_j^T f) >= -tau_max -+ bbar_j          (cpp:495,506,513)
 //   R4/R5 swing rows      +-(Js_j qdd + Js_com a) + s >= +-c'                     (cpp:496-497,507-515)
 __device__ void build_normal(const Prob& P, const double (*G)[12], const QpMap& mp, const wbc_params& pr, int p,
-                             double* n, double& b, bool& is_eq) {
+                             double* n, double& b, bool& is_eq, double& nsel, double& tolv) {
     const int kap = mp.kap;
     const int t_fr = mp.neq, t_tq = mp.neq + mp.nfr, t_sw = t_tq + mp.ntq;
     const bool in = p < mp.m;
@@ -1274,6 +1274,32 @@ __device__ void build_normal(const Prob& P, const double (*G)[12], const QpMap& 
     if (tq) b = (sg > 0) ? (-pr.max_torque - bj) : (-pr.max_torque + bj);
     if (sw) b = sg * (P.rsw[i] + (k == 2 ? g0 : 0.0));
     is_eq = eq;
+    // Selection scale and violation tolerance of the reference's own row (the 42-variable row of A
+    // at cpp:492-515 that this reduced row restates, split two-sided as qpOASES' lbA / ubA): the
+    // most violated constraint is chosen by slack / |row| in that space, as the oracle's dense
+    // active set does, so both visit the same working sets and count the same iterations
+    // (nWSR, cpp:517).  The slack itself is the same number in both spaces.
+    //   R2 friction face: |(+-1, 0, -mu)|^2 = 1 + mu^2
+    //   R3 torque row j:  |Mbar_j row j|^2 + sum over stance rows r of Jbar_c,j[r][j]^2
+    //   R4/R5 swing row i = 3 l + k: |[e_k, -S(d_l) row k]|^2 + |Jbar_j row i|^2 + 1 (the slack)
+    double s2 = 0.0;
+    if (tq) {
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+            const double mr = P.Mbj[i * 12 + j];
+            const double jc = ((kap >> (j / 3)) & 1) ? P.Jbj[j * 12 + i] : 0.0;
+            s2 = fma(mr, mr, fma(jc, jc, s2));
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 12; ++j) s2 = fma(row[j], row[j], s2);
+        const double dl2 = P.d[3 * l] * P.d[3 * l] + P.d[3 * l + 1] * P.d[3 * l + 1] + P.d[3 * l + 2] * P.d[3 * l + 2];
+        const double dk = P.d[3 * l + k];
+        s2 += 2.0 + dl2 - dk * dk;
+    }
+    nsel = fr ? 1.0 + pr.friction * pr.friction : s2;
+    const double bref = (sw && k == 2) ? b - sg * g0 : b;  // the reference row's own bound
+    tolv = 1e-10 * fmax(1.0, fabs(bref));
 }
 
 // C0[:, p] = J0^T n_p with J0 = blkdiag(I12, L^-T), in place: qdd part n, slot part L^-1 n_slot
@@ -1500,13 +1526,15 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, const Pr
 
     STAMP(a, rb, 2);
     double cc[NQ];
-    double bp = 0.0, sp = 0.0, nn = 1.0, inrm = 1.0;  // |n_p|^2, 1/|n_p|
+    double bp = 0.0, sp = 0.0, nn = 1.0, inrm = 1.0;  // |n_p|^2 (reduced), 1 / |row p| (reference space)
+    double tolv = 0.0;  // violation tolerance of row p
     double sp0 = 0.0;  // slack at the unconstrained optimum x0
     bool is_eq = false, active = false;
     const bool is_con = lane < mp.m;
     {
         EST(a, rb, 5);
-        build_normal(P, s.G, mp, pr, lane, cc, bp, is_eq);
+        double nsel;
+        build_normal(P, s.G, mp, pr, lane, cc, bp, is_eq, nsel, tolv);
         EST(a, rb, 6);
         double np[4] = {0.0, 0.0, 0.0, 0.0}, sq[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -1515,7 +1543,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, const Pr
         for (int k = 0; k < 12; ++k) sq[k & 3] += cc[12 + k] * s.xs[k];
         nn = (np[0] + np[1]) + (np[2] + np[3]);
         const double sx = (sq[0] + sq[1]) + (sq[2] + sq[3]);
-        inrm = fast_rsq(fmax(nn, 1e-300));
+        inrm = 1.0 / sqrt(fmax(nsel, 1e-300));  // selection by slack / |row| (the oracle's scale)
         sp = sx - bp;
         EST(a, rb, 7);
         to_column(s, cc);
@@ -1805,10 +1833,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, const Pr
         } else {
             if (pstar < 0) {  // most violated inequality (equalities are all active already)
                 double v = 1e300;
-                if (is_con && !is_eq && !active) {
-                    const double tol = 1e-10 * fmax(1.0, fabs(bp));
-                    if (sp < -tol) v = sp * inrm;
-                }
+                if (is_con && !is_eq && !active && sp < -tolv) v = sp * inrm;
                 const int idx = wave_argmin_lane(v);
                 if (!(bcast(v, idx) < 1e299)) break;  // no violated constraint: optimal
                 pstar = idx;
@@ -1859,7 +1884,8 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, const Pr
                 t1 = bcast(v, l1);
             }
             {
-                const double t2 = (zn > tiny) ? (-sps * fast_rcp(zn)) : 1e300;
+                // full step only along a direction the oracle also takes (zn = n^T z > 1e-14)
+                const double t2 = (zn > 1e-14) ? (-sps * fast_rcp(zn)) : 1e300;
                 const double t = fmin(t1, t2);
                 if (!(t < 1e299)) { status = WBC_QP_INFEASIBLE; break; }
                 const bool full = (t2 < 1e299 && t2 <= t1);

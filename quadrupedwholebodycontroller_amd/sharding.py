@@ -1,10 +1,27 @@
 """Batch sharding across GPUs (one process per GPU, torch.distributed over RCCL/xGMI).
 
-Robots are independent: rank g owns the contiguous range [g B/G, (g+1) B/G) and
-keeps its history resident; the only exchange is an all-gather of the torque block (and, if
-wanted, statuses) so every rank holds B x 12 torques.
+Robots are independent (the reference runs one robot per controller object,
+src/whole_body_controller.cpp:678-683): rank g owns the contiguous range [lo_g, hi_g) of
+`shard_bounds` and keeps its history resident, so the data path has no collective.  The one
+exchange is the all-gather of a step's published outputs, so that every rank holds the whole
+batch: tau (12 fp64 per robot, cpp:565-576) plus the QP status and the iteration count
+(cpp:654) as an int32 pair.
+
+`StepOutputs` is the per-rank buffer the engine writes into (wbc_bind_device_outputs) and
+`gather_step_outputs` is the single collective of a step.  bench.py calls exactly these on
+RCCL; tests/test_capi_and_dist.py drives the same functions on gloo with CPU tensors.
+
+Packed layout of one rank's block (`cap` robots, the largest shard, so every rank contributes
+the same number of bytes, as all_gather_into_tensor requires):
+
+    [ tau: cap x 12 fp64 | status: cap int32 | iters: cap int32 ]    = 13 cap doubles
+
+Rows past a rank's own shard are padding and are dropped by `unpack_gathered`.
 """
 from __future__ import annotations
+
+TAU_W = 12            # doubles of tau per robot
+ROW_DOUBLES = 13      # tau (12 fp64) + status and iters (2 int32 = 1 double's worth)
 
 
 def shard_bounds(total: int, world: int, rank: int):
@@ -12,6 +29,83 @@ def shard_bounds(total: int, world: int, rank: int):
     base, rem = divmod(total, world)
     lo = rank * base + min(rank, rem)
     return lo, lo + base + (1 if rank < rem else 0)
+
+
+def shard_capacity(total: int, world: int) -> int:
+    """Rows every rank's packed block holds: the largest shard."""
+    return -(-total // world)
+
+
+class StepOutputs:
+    """One rank's packed output block (torch tensor on the rank's device, or CPU under gloo).
+
+    tau / status / iters are views into `buf`; their data_ptr()s are what the engine binds as
+    its output buffers, so a step writes the block in place and the gather reads it directly."""
+
+    def __init__(self, cap: int, device=None):
+        import torch
+
+        self.cap = int(cap)
+        self.buf = torch.zeros(self.cap * ROW_DOUBLES, dtype=torch.float64, device=device)
+        self.tau = self.buf[: self.cap * TAU_W]
+        ints = self.buf[self.cap * TAU_W:].view(torch.int32)
+        self.status = ints[: self.cap]
+        self.iters = ints[self.cap: 2 * self.cap]
+
+    def fill(self, tau, status, iters):
+        """Copy host results of n <= cap robots into the block (CPU stand-in for a step)."""
+        import torch
+
+        n = len(status)
+        self.tau[: n * TAU_W].copy_(torch.as_tensor(tau, dtype=torch.float64).reshape(-1))
+        self.status[:n].copy_(torch.as_tensor(status, dtype=torch.int32))
+        self.iters[:n].copy_(torch.as_tensor(iters, dtype=torch.int32))
+
+
+def gather_step_outputs(block: StepOutputs, world: int, out=None, group=None):
+    """The step's one collective: every rank's packed block, concatenated in rank order
+    (RCCL all_gather_into_tensor on GPU tensors; the list form on gloo / CPU).  `out` is an
+    optional preallocated [world * 13 cap] fp64 tensor."""
+    import torch
+    import torch.distributed as dist
+
+    local = block.buf
+    if world == 1:
+        if out is not None:
+            out.copy_(local)
+            return out
+        return local
+    if out is None:
+        out = torch.empty(world * local.numel(), dtype=local.dtype, device=local.device)
+    if local.is_cuda:
+        dist.all_gather_into_tensor(out, local, group=group)
+    else:
+        parts = list(out.view(world, local.numel()).unbind(0))
+        dist.all_gather(parts, local, group=group)
+    return out
+
+
+def unpack_gathered(gathered, total: int, world: int, unit: int = 1):
+    """Gathered blocks -> (tau [total, 12], status [total], iters [total]) as numpy arrays, in
+    global robot order (padding rows of the shorter shards dropped).  Shards are whole groups of
+    `unit` rows (mode hypotheses: the K QPs of one state), cap = shard_capacity(total / unit) unit."""
+    import numpy as np
+    import torch
+
+    units = total // unit
+    cap = shard_capacity(units, world) * unit
+    g = gathered.detach().to("cpu").view(world, cap * ROW_DOUBLES)
+    taus, sts, its = [], [], []
+    for r in range(world):
+        lo, hi = shard_bounds(units, world, r)
+        n = (hi - lo) * unit
+        blk = g[r]
+        taus.append(blk[: cap * TAU_W].reshape(cap, TAU_W)[:n])
+        ints = blk[cap * TAU_W:].contiguous().view(torch.int32)
+        sts.append(ints[:n])
+        its.append(ints[cap: cap + n])
+    return (torch.cat(taus).numpy(), torch.cat(sts).numpy().astype(np.int32),
+            torch.cat(its).numpy().astype(np.int32))
 
 
 def all_gather_rows(local, world: int, group=None):

@@ -123,21 +123,31 @@ import numpy as np
 import torch, torch.distributed as dist
 sys.path.insert(0, {root!r}); sys.path.insert(0, os.path.join({root!r}, "oracle"))
 from quadrupedwholebodycontroller_amd import workloads
-from quadrupedwholebodycontroller_amd.sharding import shard_bounds, all_gather_rows
+from quadrupedwholebodycontroller_amd.sharding import (StepOutputs, gather_step_outputs, shard_bounds, shard_capacity,
+                                                       unpack_gathered)
 import wbc_ref
 dist.init_process_group("gloo")
 rank, world = dist.get_rank(), dist.get_world_size()
-B = 64
-inp = workloads.rl_random(B, seed=77)
-lo, hi = shard_bounds(B, world, rank)
-out = wbc_ref.run_batch({{k: v[lo:hi] for k, v in inp.items()}})
-tau = all_gather_rows(torch.from_numpy(out["tau"].ravel().copy()), world)
-st = all_gather_rows(torch.from_numpy(out["status"].astype(np.int64)), world)
-if rank == 0:
-    full = wbc_ref.run_batch(inp)
-    assert np.array_equal(tau.numpy().reshape(B, 12), full["tau"]), "gathered torques differ"
-    assert np.array_equal(st.numpy(), full["status"].astype(np.int64))
-    print("DIST_OK")
+# the collective bench.py runs over RCCL each step (sharding.gather_step_outputs on the packed
+# tau | status | iters block), here on CPU tensors: strong shards of an odd-sized batch (padding
+# rows), then mode-hypothesis shards in whole states (unit = K rows)
+for B, unit in ((67, 1), (5 * 4, 4)):
+    inp = workloads.rl_random(B // unit, seed=77 + unit)
+    if unit > 1:  # K = unit hypotheses per state, state-major
+        inp = {{k: np.repeat(v, unit, axis=0) for k, v in inp.items()}}
+        inp["contacts"] = np.tile(np.array([15, 5, 10, 3], np.uint8), B // unit)
+    lo, hi = shard_bounds(B // unit, world, rank)
+    lo, hi = lo * unit, hi * unit
+    out = wbc_ref.run_batch({{k: v[lo:hi] for k, v in inp.items()}}, max_torque=20.0)
+    blk = StepOutputs(shard_capacity(B // unit, world) * unit)
+    blk.fill(out["tau"], out["status"], out["iters"])
+    g = gather_step_outputs(blk, world)
+    tau, st, it = unpack_gathered(g, B, world, unit=unit)
+    if rank == 0:
+        full = wbc_ref.run_batch(inp, max_torque=20.0)
+        assert np.array_equal(tau, full["tau"]), "gathered torques differ"
+        assert np.array_equal(st, full["status"]) and np.array_equal(it, full["iters"])
+print("DIST_OK", rank)
 dist.destroy_process_group()
 """
 
@@ -150,4 +160,31 @@ def test_two_rank_gloo_shard_and_gather(tmp_path):
            "--master-addr=127.0.0.1", "--master-port=29531", str(script)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
-    assert "DIST_OK" in r.stdout
+    assert "DIST_OK 0" in r.stdout and "DIST_OK 1" in r.stdout
+
+
+def test_bench_world_mismatch_exits_nonzero():
+    """bench.py --gpus N inside a torch.distributed environment of another size refuses to run
+    (it never reports n_gpus different from what was asked)."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=1 but --gpus 2" in r.stderr
+
+
+def test_bench_strong_shards_cover_the_global_batch():
+    """Strong scaling: the ranks' input shards concatenate to the global batch of the config (so
+    the gathered outputs are the same for every N); mode hypotheses shard by whole state."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    for name in ("rl_random_b65536", "modes16_x8192"):
+        cfg = dict(bench.CONFIGS[name])
+        K = cfg.get("modes", 0) or 1
+        cfg["batch"] = 96 * K  # small stand-in of the same generator
+        _, _, ref, _, tot = bench.shard_inputs(cfg, "strong", 1, 0)
+        for world in (2, 3, 8):
+            parts = [bench.shard_inputs(cfg, "strong", world, r) for r in range(world)]
+            assert sum(p[0] for p in parts) == tot == 96 * K
+            for k in ref:
+                assert np.array_equal(np.concatenate([p[2][k] for p in parts]), ref[k]), (name, world, k)
