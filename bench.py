@@ -258,12 +258,20 @@ def main():
 
     import torch
 
+    # WBC_DIST_BACKEND=gloo rehearses the N-rank path on a box with fewer GPUs (ranks share
+    # devices, the gather goes through the host); the measured path is nccl (= RCCL over xGMI)
+    backend = os.environ.get("WBC_DIST_BACKEND", "nccl")
+    if backend == "gloo":
+        local_rank %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
 
     from quadrupedwholebodycontroller_amd import FUSED, NO_X, STATELESS, Engine
     from quadrupedwholebodycontroller_amd.sharding import (StepOutputs, gather_step_outputs, shard_capacity,

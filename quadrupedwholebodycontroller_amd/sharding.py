@@ -77,8 +77,12 @@ def gather_step_outputs(block: StepOutputs, world: int, out=None, group=None):
         return local
     if out is None:
         out = torch.empty(world * local.numel(), dtype=local.dtype, device=local.device)
-    if local.is_cuda:
+    if local.is_cuda and dist.get_backend(group) != "gloo":
         dist.all_gather_into_tensor(out, local, group=group)
+    elif local.is_cuda:  # gloo rehearsal of the GPU path (several ranks on one device): via host
+        host = torch.empty(out.numel(), dtype=out.dtype)
+        dist.all_gather(list(host.view(world, local.numel()).unbind(0)), local.cpu(), group=group)
+        out.copy_(host)
     else:
         parts = list(out.view(world, local.numel()).unbind(0))
         dist.all_gather(parts, local, group=group)
