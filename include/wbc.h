@@ -154,7 +154,8 @@ int32_t wbc_create(const wbc_model* model, const wbc_params* params, int32_t bat
                    wbc_engine** out);
 int32_t wbc_destroy(wbc_engine* h);
 int32_t wbc_batch(const wbc_engine* h);
-/* Use a caller-owned hipStream_t (NULL = the engine's own stream). */
+/* Use a caller-owned hipStream_t (NULL = the engine's own stream).  Work queued on the previous
+ * stream is drained first (the call synchronizes it), so switching streams never races. */
 int32_t wbc_set_stream(wbc_engine* h, void* hip_stream);
 
 /* Host inputs, copied to device on the engine stream. Any pointer may be NULL (= unchanged). */
@@ -202,13 +203,19 @@ int32_t wbc_step_modes(wbc_engine* h, uint32_t flags);
  * and sent in one H2D copy, the step runs (flags as wbc_step), and the outputs come back in one D2H
  * copy and one synchronize.  Same results as wbc_set_state + wbc_set_reference + wbc_step +
  * wbc_get_output.  Inputs are all required; any output may be NULL (x NULL also skips computing
- * it, as WBC_NO_X).  Refused while mode hypotheses are set. */
+ * it, as WBC_NO_X).  Input and output bindings (wbc_bind_device_*) are left as they were: the
+ * cycle reads and writes the engine's own buffers for this one step.  Refused while mode
+ * hypotheses are set. */
 int32_t wbc_cycle(wbc_engine* h, const double* base_pose, const double* nu, const double* qj, const double* ref,
                   const uint8_t* contacts, const uint8_t* switching, uint32_t flags, double* tau, double* grf,
                   double* x, int32_t* status, int32_t* iters);
 
 /* Outputs (host copies, synchronous).  Any pointer may be NULL.
- * tau [B][12], grf [B][12] (= x[18:30]), x [B][42], status [B], iters [B]. */
+ * tau [B][12], grf [B][12] (= x[18:30]), x [B][42], status [B], iters [B].
+ * A robot whose status is not WBC_QP_OK gets tau, grf and x all zero (the reference publishes
+ * qpOASES' last iterate and then stops its control loop, cpp:652-659; a batch keeps running, so
+ * a failed robot publishes zeros instead of an unconverged iterate).  iters is the cap
+ * (max_wsr) under WBC_QP_MAX_ITER. */
 int32_t wbc_get_output(wbc_engine* h, double* tau, double* grf, double* x, int32_t* status,
                        int32_t* iters);
 /* Device pointers of the output buffers (valid until wbc_destroy). */

@@ -153,7 +153,9 @@ void WholeBodyController::controlCycle() {
 }
 
 void WholeBodyController::publish() {
-    // published before the caller checks the QP status, as in the reference (cpp:652-659)
+    // published before the caller checks the QP status, in the reference's order (cpp:652-659).
+    // One difference: on a failed solve the reference publishes qpOASES' last iterate, the engine
+    // publishes zeros (wbc.h, wbc_get_output); controlLoop then terminates either way.
     if (desiredGroundReactionForcesPublisher) {
         Float64MultiArray g;
         g.data.assign(grf_.begin(), grf_.end());

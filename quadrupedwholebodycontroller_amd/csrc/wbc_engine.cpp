@@ -252,7 +252,9 @@ int32_t wbc_create(const wbc_model* model, const wbc_params* params, int32_t bat
 int32_t wbc_destroy(wbc_engine* h) {
     if (!h) return WBC_OK;
     (void)hipSetDevice(h->device);
-    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    // drain in-flight work before freeing: the device, not h->stream, which may be a caller's
+    // stream that was already destroyed
+    (void)hipDeviceSynchronize();
     void* ptrs[] = {h->d_model, h->d_params, h->d_inblk, h->d_outblk, h->d_mask, h->d_modes, h->d_hist, h->d_work,
                     h->d_dbg};
     for (void* p : ptrs)
@@ -270,7 +272,14 @@ int32_t wbc_batch(const wbc_engine* h) { return h ? h->batch : 0; }
 
 int32_t wbc_set_stream(wbc_engine* h, void* stream) {
     if (!h) return fail(WBC_ERR_ARG, "null handle");
-    h->stream = stream ? reinterpret_cast<hipStream_t>(stream) : h->own_stream;
+    const hipStream_t next = stream ? reinterpret_cast<hipStream_t>(stream) : h->own_stream;
+    if (next != h->stream) {
+        // work already queued on the old stream still reads the engine's buffers: let it finish
+        // before any call on the new stream can overwrite them
+        WBC_HIP(hipSetDevice(h->device));
+        WBC_HIP(hipStreamSynchronize(h->stream));
+    }
+    h->stream = next;
     return WBC_OK;
 }
 
@@ -441,6 +450,9 @@ int32_t wbc_cycle(wbc_engine* h, const double* base_pose, const double* nu, cons
     std::memcpy(reinterpret_cast<uint8_t*>(hp), contacts, B);
     std::memcpy(reinterpret_cast<uint8_t*>(hp) + B, switching, B);
     WBC_HIP(hipMemcpyAsync(h->d_inblk, h->h_in, inb, hipMemcpyHostToDevice, h->stream));
+    // inputs from the engine's own block for this step only (caller bindings are restored after)
+    const double* const ip = h->in_pose; const double* const in = h->in_nu; const double* const iq = h->in_qj;
+    const double* const ir = h->in_ref; const uint8_t* const ic = h->in_contacts; const uint8_t* const is = h->in_switching;
     h->in_pose = h->d_pose;
     h->in_nu = h->d_nu;
     h->in_qj = h->d_qj;
@@ -454,6 +466,7 @@ int32_t wbc_cycle(wbc_engine* h, const double* base_pose, const double* nu, cons
     if (!x) flags |= WBC_NO_X;
     const int32_t rc = wbc_step(h, flags);
     h->out_tau = bt; h->out_grf = bg; h->out_x = bx; h->out_status = bs; h->out_iters = bi;
+    h->in_pose = ip; h->in_nu = in; h->in_qj = iq; h->in_ref = ir; h->in_contacts = ic; h->in_switching = is;
     if (rc != WBC_OK) return rc;
     // one D2H copy (x, last in the block, only when asked for)
     const size_t xb = B * WBC_NV * sizeof(double);

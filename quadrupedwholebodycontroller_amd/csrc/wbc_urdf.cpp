@@ -7,13 +7,16 @@
 // name, and the foot frame is located by name inside the last body.  Same algorithm as
 // tools/gen_model.py (which produced the committed ANYmal constants).  A small XML reader is
 // included: URDF needs elements and attributes only.
+#include <cerrno>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
 #include <map>
 #include <memory>
 #include <sstream>
+#include <stdexcept>
 #include <string>
 #include <tuple>
 #include <vector>
@@ -131,21 +134,38 @@ M3 rpy(double r, double p, double y) {  // URDF: R = Rz(yaw) Ry(pitch) Rx(roll)
     Rz.a[0] = cos(y); Rz.a[1] = -sin(y); Rz.a[3] = sin(y); Rz.a[4] = cos(y);
     return mul(mul(Rz, Ry), Rx);
 }
-std::vector<double> nums(const std::string& s) {
+// Strict numeric attributes: exactly `n` whitespace-separated numbers, nothing else (a malformed
+// attribute is an error, never a silent zero or identity).
+struct UrdfError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+std::vector<double> nums(const std::string& s, size_t n, const char* what) {
     std::vector<double> v;
-    std::istringstream is(s);
-    double x;
-    while (is >> x) v.push_back(x);
+    const char* p = s.c_str();
+    for (;;) {
+        while (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r') ++p;
+        if (!*p) break;
+        char* end = nullptr;
+        errno = 0;
+        const double x = std::strtod(p, &end);
+        if (end == p || errno == ERANGE || !std::isfinite(x))
+            throw UrdfError(std::string("malformed number in ") + what + "=\"" + s + "\"");
+        v.push_back(x);
+        p = end;
+    }
+    if (v.size() != n)
+        throw UrdfError(std::string(what) + "=\"" + s + "\" must hold " + std::to_string(n) + " number(s)");
     return v;
 }
+double num1(const std::string& s, const char* what) { return nums(s, 1, what)[0]; }
 void origin(const Xml* o, M3& R, V3& p) {
     R = M3();
     p = V3();
     if (!o) return;
-    const auto xyz = nums(o->get("xyz", "0 0 0"));
-    const auto r = nums(o->get("rpy", "0 0 0"));
-    if (xyz.size() == 3) p = V3{{xyz[0], xyz[1], xyz[2]}};
-    if (r.size() == 3) R = rpy(r[0], r[1], r[2]);
+    const auto xyz = nums(o->get("xyz", "0 0 0"), 3, "origin xyz");
+    const auto r = nums(o->get("rpy", "0 0 0"), 3, "origin rpy");
+    p = V3{{xyz[0], xyz[1], xyz[2]}};
+    R = rpy(r[0], r[1], r[2]);
 }
 
 struct Inertial {
@@ -234,8 +254,8 @@ int32_t err(const std::string& m) {
 
 }  // namespace
 
-extern "C" int32_t wbc_model_from_urdf(const char* path, const char* const* legs, const char* const* joints,
-                                       const char* foot_suffix, wbc_model* out) {
+static int32_t model_from_urdf(const char* path, const char* const* legs, const char* const* joints,
+                               const char* foot_suffix, wbc_model* out) {
     if (!path || !out) return err("wbc_model_from_urdf: null argument");
     std::ifstream f(path);
     if (!f) return err(std::string("wbc_model_from_urdf: cannot open ") + path);
@@ -257,8 +277,9 @@ extern "C" int32_t wbc_model_from_urdf(const char* path, const char* const* legs
                 const Xml* m = ie->child("mass");
                 const Xml* a = ie->child("inertia");
                 if (!m || !a) return err("wbc_model_from_urdf: incomplete <inertial> in link " + el->get("name"));
-                in.m = std::stod(m->get("value", "0"));
-                auto g = [&](const char* k) { return std::stod(a->get(k, "0")); };
+                in.m = num1(m->get("value", "0"), "mass value");
+                if (!(in.m >= 0.0)) return err("wbc_model_from_urdf: negative mass in link " + el->get("name"));
+                auto g = [&](const char* k) { return num1(a->get(k, "0"), k); };
                 M3 I{{g("ixx"), g("ixy"), g("ixz"), g("ixy"), g("iyy"), g("iyz"), g("ixz"), g("iyz"), g("izz")}};
                 in.c = p;
                 in.I = mul(mul(R, I), transpose(R));
@@ -277,8 +298,10 @@ extern "C" int32_t wbc_model_from_urdf(const char* path, const char* const* legs
             origin(el->child("origin"), j.R, j.p);
             j.axis = V3{{1, 0, 0}};
             if (const Xml* ax = el->child("axis")) {
-                const auto v = nums(ax->get("xyz"));
-                if (v.size() == 3) j.axis = V3{{v[0], v[1], v[2]}};
+                const auto v = nums(ax->get("xyz"), 3, "axis xyz");
+                const double n = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+                if (!(n > 1e-12)) return err("wbc_model_from_urdf: zero joint axis in " + j.name);
+                j.axis = V3{{v[0] / n, v[1] / n, v[2] / n}};  // URDF axes are unit vectors; normalise
             }
             rb.joints[j.name] = j;
             rb.joint_order.push_back(j.name);
@@ -313,6 +336,11 @@ extern "C" int32_t wbc_model_from_urdf(const char* path, const char* const* legs
     for (int i = 0; i < 3; ++i) m.base_com[i] = bc.inert.c.v[i];
     for (int k = 0; k < 9; ++k) m.base_inertia[k] = bc.inert.I.a[k];
     double total = bc.inert.m;
+    // every moving joint off the base must be a leg's first joint: anything else (an arm, a
+    // second chain) would carry mass the lumped 12-DoF model cannot represent
+    if (bc.out.size() != 4)
+        return err("wbc_model_from_urdf: " + std::to_string(bc.out.size()) +
+                   " moving joints leave the base (expected the 4 leg roots)");
     for (int l = 0; l < 4; ++l) {
         std::string jn = std::string(L[l]) + "_" + J[0];
         Frame fr;
@@ -336,6 +364,9 @@ extern "C" int32_t wbc_model_from_urdf(const char* path, const char* const* legs
                 for (const auto& o : c.out)
                     if (o.first == nxt) { fr = o.second; ++cnt; }
                 if (cnt != 1) return err("wbc_model_from_urdf: joint " + nxt + " does not follow " + jn);
+                if (c.out.size() != 1)
+                    return err("wbc_model_from_urdf: link after " + jn + " has " + std::to_string(c.out.size()) +
+                               " moving child joints (a leg is one chain)");
                 jn = nxt;
             } else {
                 if (!c.out.empty()) return err("wbc_model_from_urdf: leg " + std::string(L[l]) + " has more than 3 joints");
@@ -349,4 +380,17 @@ extern "C" int32_t wbc_model_from_urdf(const char* path, const char* const* legs
     m.total_mass = total;  // model_.getTotalMass(), cpp:72
     *out = m;
     return WBC_OK;
+}
+
+// No exception crosses the C boundary (wbc.h): malformed numbers and allocation failures become
+// WBC_ERR_ARG with the message in wbc_last_error().
+extern "C" int32_t wbc_model_from_urdf(const char* path, const char* const* legs, const char* const* joints,
+                                       const char* foot_suffix, wbc_model* out) {
+    try {
+        return model_from_urdf(path, legs, joints, foot_suffix, out);
+    } catch (const std::exception& e) {
+        return err(std::string("wbc_model_from_urdf: ") + e.what());
+    } catch (...) {
+        return err("wbc_model_from_urdf: unknown error");
+    }
 }

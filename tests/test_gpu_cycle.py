@@ -63,3 +63,25 @@ def test_cycle_keeps_bound_outputs_and_refuses_modes():
     with pytest.raises(WbcError):
         e.cycle(inp["base_pose"], inp["nu"], inp["qj"], inp["ref"], inp["contacts"], inp["switching"], STATELESS)
     e.close()
+
+
+def test_cycle_keeps_bound_inputs():
+    """A caller that bound device inputs keeps them across wbc_cycle: the cycle reads its own host
+    arrays for that one step, the next plain step reads the bound tensors again."""
+    import torch
+
+    B = 24
+    a, b = workloads.rl_random(B, seed=61), workloads.rl_random(B, seed=62)
+    want_a = separate_calls(Engine(B), a, STATELESS)
+    want_b = separate_calls(Engine(B), b, STATELESS)
+    d = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in a.items()}
+    e = Engine(B)
+    e.bind_device_inputs(d["base_pose"].data_ptr(), d["nu"].data_ptr(), d["qj"].data_ptr(), d["ref"].data_ptr(),
+                         d["contacts"].data_ptr(), d["switching"].data_ptr())
+    got_b = e.cycle(b["base_pose"], b["nu"], b["qj"], b["ref"], b["contacts"], b["switching"], STATELESS)
+    e.step(STATELESS)
+    got_a = e.outputs()
+    e.close()
+    for k in KEYS:
+        assert np.array_equal(got_b[k], want_b[k]), k
+        assert np.array_equal(got_a[k], want_a[k]), k

@@ -112,3 +112,39 @@ def test_loader_errors(tmp_path):
         fh.write('<robot name="x"><link name="a"></robot>')
     with pytest.raises(WbcError):
         model_from_urdf(bad)
+
+
+def test_loader_rejects_malformed_numbers_and_extra_chains(tmp_path):
+    """Malformed attributes are errors, not silent zeros (no exception escapes the C-ABI: the
+    process survives and WbcError carries the message); chains the lumped model cannot hold
+    (an extra moving joint off the base or mid-leg) are refused instead of dropping their mass."""
+    import re
+
+    names = dict(legs=("FL", "FR", "HL", "HR"), joints=("hip_roll", "hip_pitch", "knee"), foot_suffix="toe")
+    p = str(tmp_path / "q.urdf")
+    synthetic_urdf(p, 5, names["legs"], names["joints"], names["foot_suffix"])
+    good = open(p).read()
+    model_from_urdf(p, **names)  # the unmodified robot loads
+
+    def bad(text, match):
+        q = str(tmp_path / "bad.urdf")
+        with open(q, "w") as fh:
+            fh.write(text)
+        with pytest.raises(WbcError, match=match):
+            model_from_urdf(q, **names)
+
+    bad(re.sub(r'<mass value="[^"]*"', '<mass value="abc"', good, count=1), "malformed number")
+    bad(re.sub(r'<origin xyz="[^"]*"', '<origin xyz="0.1 0.2"', good, count=1), "must hold 3")
+    bad(re.sub(r'rpy="[^"]*"', 'rpy="0 0 0 x"', good, count=1), "malformed number")
+    bad(re.sub(r'<axis xyz="[^"]*"', '<axis xyz="0 0 0"', good, count=1), "zero joint axis")
+    bad(re.sub(r'<axis xyz="[^"]*"', '<axis xyz="1 0"', good, count=1), "must hold 3")
+    m = re.search(r'<joint name="FL_hip_roll".*?</joint>', good, re.S)
+    root = re.search(r'<parent link="([^"]+)"', m.group(0)).group(1)
+    arm = (f'<link name="arm"><inertial><mass value="2.0"/><inertia ixx="0.1" ixy="0" ixz="0" iyy="0.1" iyz="0" '
+           f'izz="0.1"/></inertial></link><joint name="arm_joint" type="revolute"><parent link="{root}"/>'
+           f'<child link="arm"/><axis xyz="0 0 1"/></joint></robot>')
+    bad(good.replace("</robot>", arm), "moving joints leave the base")
+    thigh = re.search(r'<child link="([^"]+)"', re.search(r'<joint name="FL_hip_pitch".*?</joint>', good, re.S)
+                      .group(0)).group(1)
+    extra = arm.replace(f'<parent link="{root}"/>', f'<parent link="{thigh}"/>')
+    bad(good.replace("</robot>", extra), "moving child joints")
