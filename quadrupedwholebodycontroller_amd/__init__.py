@@ -5,8 +5,13 @@ computeJointTorques, src/whole_body_controller.cpp:650-652) as hand-written HIP 
 behind the C-ABI in include/wbc.h.  This package is the Python view of that C-ABI:
 
   Engine          batched handle (wbc_create ... wbc_get_output), see _capi.py
+  Planner         batched motion planner (WbcReferenceMsg producer), see _capi.py
   workloads       synthetic inputs of the BASELINE.json configurations
-  controller      WholeBodyController-shaped single-robot shim over the engine
+  sharding        robot shards and the per-step all-gather of the multi-GPU path
+  ros_wire        ROS1 wire-byte adapters (libwbc_ros.so)
+
+The WholeBodyController-shaped single-robot shim is C++ (include/wbc_controller.hpp,
+libwbc_controller.so), as the reference's class is.
 
 The product path has no CPU fallback: without libwbc_hip.so or a GPU it raises.
 """

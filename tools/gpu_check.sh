@@ -24,6 +24,9 @@ for s in ${STEPS:-smoke pytest bench prof}; do
     stamps2) step stamps2 300 env WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_stamps.so python tools/stamps.py rl_random 8192 ;;
     split) step split 600 python tools/split_probe.py 30 ${VARIANTS:-uw2,uw3,uw4} ;;
     variants) step variants 600 python tools/variants.py 30 ${VARIANTS:-w2,w3,w4,w5} ;;
+    dist)   step dist 400 env WBC_DIST_BACKEND=gloo python bench.py --gpus 2 --config rl_random_b65536 --steps 10 --warmup 2 ;;
+    strong1) step strong1 400 python bench.py --config rl_random_b65536 --steps 10 --warmup 2 --no-cpu-baseline ;;
+    extra)  step extra 400 python bench.py --steps 20 --warmup 3 --extra --no-cpu-baseline ;;
     counters) step counters 120 rocprofv3 -L ;;
     pmc)    step pmc 1200 bash tools/pmc.sh ;;
     prof)   step prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o $TAG --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
