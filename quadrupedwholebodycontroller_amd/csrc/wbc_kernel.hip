@@ -73,6 +73,7 @@ struct UpdScratch {
 };
 
 struct QpScratch {
+    static constexpr int N = NQ;
     double L[12][13];       // Cholesky factor of the slot Hessian (row-major, lower); then M = L^-1
     __device__ double (&Mi())[12][12] { return *reinterpret_cast<double(*)[12][12]>(&L[0][0]); }
     double xs[12];          // slot part of x0 = -H^-1 g
@@ -90,6 +91,19 @@ struct QpScratch {
     // R^-1 (upper triangular, zero elsewhere): element (i, j) at Rv[j / 2][i].{x, y}[j % 2], so
     // lane i reads its row as 12 conflict-free ds_read_b128 and R^-1 d needs no masking
     double2 Rv[NQ / 2][NQ];
+};
+
+// Scratch of the four-contact stance solve (12 force variables, 40 inequality rows; wbc_layout.h)
+struct StanceScratch {
+    static constexpr int N = 12;
+    static constexpr int MC = 40;  // 16 friction faces + 24 torque rows
+    double M_[12][12];      // M = L^-1 of H_f (lower)
+    __device__ double (&Mi())[12][12] { return M_; }
+    double xs[12];          // f0 = -H_f^-1 g_f
+    double colbuf[16];      // hotstart slot -> constraint exchange
+    double ucon[24];        // after the loop: f (0..11), qdd (12..23)
+    double2 c0[N / 2][MC];  // initial columns C0[:, p] = M n_p
+    double2 Rv[N / 2][N];   // R^-1, as in QpScratch
 };
 
 struct Lds {
@@ -292,6 +306,10 @@ __device__ __forceinline__ bool seg_any(bool p) {
 #ifndef WBC_XCD_REMAP
 #define WBC_XCD_REMAP 0
 #endif
+// Four-contact stance solved in the 12-variable force space (Presolve::stance, wbc_layout.h)
+#ifndef WBC_STANCE_ELIM
+#define WBC_STANCE_ELIM 1
+#endif
 __device__ __forceinline__ int xcd_robot() {
     if (!WBC_XCD_REMAP) return blockIdx.x;
     constexpr int NXCD = 8;
@@ -454,43 +472,42 @@ __device__ __forceinline__ void g_row(const Prob& P, int i, double* grow) {
 
 // The part of solveQP (cpp:466-515) that depends on the contact mask but not on the constraints:
 // the slot Hessian H_s = I + Jc_com (I + Mbar_b^-2) Jc_com^T on stance slots (slack_weight I on
-// swing slots; lane i < 12 of the robot's segment holds row i), its Cholesky factor, M = L^-1
-// (lower, written over L) and x0's slot part xs = -H_s^-1 g_s.  Runs at the end of the update (four
-// robots per wave in the update kernel) or, under mode hypotheses, in the solve.  Returns false
-// when H_s is not positive definite.
-template <int SUB>
-__device__ bool presolve(const Prob& P, int kap, const wbc_params& pr, int lane, double (&L)[12][13], double* ild,
-                         double* xs) {
+// swing slots; lane i < 12 of the robot's segment holds row i) and the slot gradient
+// g_s = -Jc_com (W + [0, 0, g/m, 0, 0, 0]).
+__device__ __forceinline__ void slot_hessian_row(const Prob& P, int kap, const wbc_params& pr, int lane,
+                                                 double (&hrow)[12], double& gsv) {
     const double inv_m = P.inv_m;
-    double hrow[12];
-    double gsv = 0.0;
-    {
-        const int i = lane < 12 ? lane : 11, li = i / 3, ri = i % 3;
-        const bool sti = (kap >> li) & 1;
-        const double di[3] = {P.d[3 * li], P.d[3 * li + 1], P.d[3 * li + 2]};
-        double e[3] = {ri == 0 ? 1.0 : 0.0, ri == 1 ? 1.0 : 0.0, ri == 2 ? 1.0 : 0.0}, ui[3];
-        cross3(di, e, ui);
-        double t[3], t2[3], Gu[3];
-        mv3(P.Icinv, ui, t);
-        mv3(P.Icinv, t, t2);
-        Gu[0] = ui[0] + t2[0]; Gu[1] = ui[1] + t2[1]; Gu[2] = ui[2] + t2[2];
-        const double ims = 1.0 + inv_m * inv_m;
+    const int i = lane < 12 ? lane : 11, li = i / 3, ri = i % 3;
+    const bool sti = (kap >> li) & 1;
+    const double di[3] = {P.d[3 * li], P.d[3 * li + 1], P.d[3 * li + 2]};
+    double e[3] = {ri == 0 ? 1.0 : 0.0, ri == 1 ? 1.0 : 0.0, ri == 2 ? 1.0 : 0.0}, ui[3];
+    cross3(di, e, ui);
+    double t[3], t2[3], Gu[3];
+    mv3(P.Icinv, ui, t);
+    mv3(P.Icinv, t, t2);
+    Gu[0] = ui[0] + t2[0]; Gu[1] = ui[1] + t2[1]; Gu[2] = ui[2] + t2[2];
+    const double ims = 1.0 + inv_m * inv_m;
 #pragma unroll
-        for (int lj = 0; lj < 4; ++lj) {
-            const bool stj = (kap >> lj) & 1;
-            const double dj[3] = {P.d[3 * lj], P.d[3 * lj + 1], P.d[3 * lj + 2]};
-            double hc[3];
-            cross3(Gu, dj, hc);
+    for (int lj = 0; lj < 4; ++lj) {
+        const bool stj = (kap >> lj) & 1;
+        const double dj[3] = {P.d[3 * lj], P.d[3 * lj + 1], P.d[3 * lj + 2]};
+        double hc[3];
+        cross3(Gu, dj, hc);
 #pragma unroll
-            for (int rj = 0; rj < 3; ++rj) {
-                const int j = 3 * lj + rj;
-                const double h = (i == j ? 1.0 : 0.0) + (ri == rj ? ims : 0.0) + hc[rj];
-                hrow[j] = (sti && stj) ? h : ((!sti && i == j) ? pr.slack_weight : 0.0);
-            }
+        for (int rj = 0; rj < 3; ++rj) {
+            const int j = 3 * lj + rj;
+            const double h = (i == j ? 1.0 : 0.0) + (ri == rj ? ims : 0.0) + hc[rj];
+            hrow[j] = (sti && stj) ? h : ((!sti && i == j) ? pr.slack_weight : 0.0);
         }
-        // g_s = -Jc_com (W + [0, 0, g/m, 0, 0, 0])
-        gsv = sti ? -(P.W[ri] + (ri == 2 ? pr.gravity * inv_m : 0.0) + dot3(ui, &P.W[3])) : 0.0;
     }
+    gsv = sti ? -(P.W[ri] + (ri == 2 ? pr.gravity * inv_m : 0.0) + dot3(ui, &P.W[3])) : 0.0;
+}
+
+// Cholesky factor of a 12 x 12 SPD matrix (row i in lane i of the robot's segment, as hrow), its
+// inverse M = L^-1 (lower, written over L) and x0 = -H^-1 g (g_i in lane i).  Returns false when
+// the matrix is not positive definite.
+template <int SUB>
+__device__ bool factor12(double (&hrow)[12], double gsv, int lane, double (&L)[12][13], double* ild, double* xs) {
     // right-looking Cholesky, row i in lane i; L_jk broadcast from lane j of the segment
     bool chol_ok = true;
     double ildv = 1.0;  // lane k: 1 / L_kk
@@ -532,7 +549,7 @@ __device__ bool presolve(const Prob& P, int kap, const wbc_params& pr, int lane,
         }
     }
     lds_sync();
-    // x0 = -H_s^-1 g_s = -M^T (M g_s): g_k and z_k broadcast from lane k
+    // x0 = -H^-1 g = -M^T (M g): g_k and z_k broadcast from lane k
     {
         double gk[12];
 #pragma unroll
@@ -549,6 +566,144 @@ __device__ bool presolve(const Prob& P, int kap, const wbc_params& pr, int lane,
     }
     lds_sync();
     return chol_ok;
+}
+
+// Slot factorisation of the general solve: H_s, its factor, M = L^-1 and x0's slot part.  Runs
+// at the end of the update (four robots per wave in the update kernel) or, under mode
+// hypotheses, in the solve.  Returns false when H_s is not positive definite.
+template <int SUB>
+__device__ bool presolve(const Prob& P, int kap, const wbc_params& pr, int lane, double (&L)[12][13], double* ild,
+                         double* xs) {
+    double hrow[12], gsv;
+    slot_hessian_row(P, kap, pr, lane, hrow, gsv);
+    return factor12<SUB>(hrow, gsv, lane, L, ild, xs);
+}
+
+// Maximum over each 16-lane DPP row (row_ror 8/4/2/1 leaves it in every lane of the row).
+__device__ __forceinline__ double seg16_max(double v) {
+    v = fmax(v, dpp_d<0x128>(v));
+    v = fmax(v, dpp_d<0x124>(v));
+    v = fmax(v, dpp_d<0x122>(v));
+    v = fmax(v, dpp_d<0x121>(v));
+    return v;
+}
+// Index (within the row) of the lane of each 16-lane DPP row holding the largest v >= 0, ties to
+// the lowest lane: the lane index is written into the 4 low mantissa bits before the max.
+__device__ __forceinline__ int seg16_argmax(double v) {
+    const int tag = 15 - ((int)threadIdx.x & 15);
+    v = seg16_max(__hiloint2double(__double2hiint(v), (__double2loint(v) & ~15) | tag));
+    return 15 - (__double2loint(v) & 15);
+}
+
+// Four-contact stance (kappa = 15): eliminate the 12 stance equalities Jbj qdd + G f = e (R1,
+// cpp:494,504; G = Jc_com Mbar_b^-1 Jc_com^T, e = r1 + g e_z) as qdd = q0 - P f by Gauss-Jordan
+// with partial pivoting on [Jbj | G | e] (row i in lane i), then form the force-space Hessian
+// row H_f = P^T P + H_s and gradient g_f = g_s - P^T q0 (returned in hrow / gsv for factor12),
+// the torque map Nt = Mbj P + Jbj^T, t0 = bbj + Mbj q0 and the torque rows' reference-space
+// norms; P, q0, Nt, t0 and nsel go straight to the Presolve record.  X aliases the factor's L
+// area (its lifetime ends before the factorisation), piv the ild / xs area.  Returns false
+// (nothing stored; the caller takes the general path) when a pivot is below 1e-9 of the largest
+// entry of Jbj.  SUB = 16 only (one robot per DPP row).
+__device__ bool stance_reduce(const Prob& P, const wbc_params& pr, int lane, bool wr, double (&X)[12][13],
+                              double* piv, double (&hrow)[12], double& gsv, Presolve* pre) {
+    const int i = lane < 12 ? lane : 11;
+    double a[12], rhs[13];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) a[j] = P.Jbj[i * 12 + j];
+    g_row(P, i, rhs);
+    rhs[12] = P.r1[i] + ((i % 3) == 2 ? pr.gravity : 0.0);
+    double amax = 0.0;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) amax = fmax(amax, fabs(a[j]));
+    bool pivoted = lane >= 12;
+    int my_step = 0;
+    double min_piv = 1e300;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        const int p = seg16_argmax(pivoted ? 0.0 : fabs(a[k]));
+        if (lane == p) {
+            // pivot row: columns k+1..11 of the Jbj part at piv[c - 1], the 13 right-hand sides at 11..23
+#pragma unroll
+            for (int c = k + 1; c < 12; ++c) piv[c - 1] = a[c];
+#pragma unroll
+            for (int c = 0; c < 13; ++c) piv[11 + c] = rhs[c];
+            my_step = k;
+            pivoted = true;
+        }
+        const double pa = __shfl(a[k], ((int)threadIdx.x & ~15) + p);
+        lds_sync();
+        const double ip = 1.0 / pa;
+        min_piv = fmin(min_piv, fabs(pa));
+        const double fct = (lane == p) ? 0.0 : a[k] * ip;
+        const double own = (lane == p) ? ip : 1.0;
+#pragma unroll
+        for (int c = k + 1; c < 12; ++c) a[c] = fma(-fct, piv[c - 1], a[c] * own);
+#pragma unroll
+        for (int c = 0; c < 13; ++c) rhs[c] = fma(-fct, piv[11 + c], rhs[c] * own);
+        lds_sync();  // the next pivot row overwrites piv
+    }
+    const double am = seg16_max(amax);
+    // min_piv is uniform over the segment; a pivot this small relative to the matrix means a leg
+    // at (or near) a singular configuration: the general path handles it
+    const bool ok = min_piv > 1e-9 * am;
+    // lane i holds row my_step of X = Jbj^-1 [G | e]: P (12) and q0
+    if (lane < 12) {
+#pragma unroll
+        for (int c = 0; c < 13; ++c) X[my_step][c] = rhs[c];
+    }
+    lds_sync();
+    // lane j < 12: column j of P (H_f row j, g_f), row j of Nt (torque joint j); X and the
+    // problem are read from LDS inside the loops (few values live across them)
+    const int j = i;
+    slot_hessian_row(P, 15, pr, lane, hrow, gsv);
+    {
+        double pcol[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) pcol[k] = X[k][j];
+        double gq[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k = 0; k < 12; ++k) gq[k & 3] = fma(pcol[k], X[k][12], gq[k & 3]);
+        gsv -= (gq[0] + gq[1]) + (gq[2] + gq[3]);
+#pragma unroll
+        for (int c = 0; c < 12; ++c) {
+            double h4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int k = 0; k < 12; ++k) h4[k & 3] = fma(pcol[k], X[k][c], h4[k & 3]);
+            hrow[c] += (h4[0] + h4[1]) + (h4[2] + h4[3]);
+        }
+    }
+    // Nt row j = Mbj row j . P + Jbj column j; t0_j = bbj_j + Mbj row j . q0
+    double t4[4] = {0.0, 0.0, 0.0, 0.0}, s2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        const double mk = P.Mbj[j * 12 + k], jc = P.Jbj[k * 12 + j];
+        t4[k & 3] = fma(mk, X[k][12], t4[k & 3]);
+        s2 = fma(mk, mk, fma(jc, jc, s2));
+    }
+    const double t0 = P.bbj[j] + ((t4[0] + t4[1]) + (t4[2] + t4[3]));
+#pragma unroll 1
+    for (int c = 0; c < 12; c += 2) {  // not unrolled: unrolled, the X reads of all columns are hoisted (spills)
+        double n0[4] = {0.0, 0.0, 0.0, 0.0}, n1[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k = 0; k < 12; ++k) {
+            const double mk = P.Mbj[j * 12 + k];
+            n0[k & 3] = fma(mk, X[k][c], n0[k & 3]);
+            n1[k & 3] = fma(mk, X[k][c + 1], n1[k & 3]);
+        }
+        const double v0 = P.Jbj[c * 12 + j] + ((n0[0] + n0[1]) + (n0[2] + n0[3]));
+        const double v1 = P.Jbj[(c + 1) * 12 + j] + ((n1[0] + n1[1]) + (n1[2] + n1[3]));
+        if (ok && wr && lane < 12) {
+            *reinterpret_cast<double2*>(&pre->Nt[j * 12 + c]) = make_double2(v0, v1);
+            *reinterpret_cast<double2*>(&pre->P[j * 12 + c]) = make_double2(X[j][c], X[j][c + 1]);
+        }
+    }
+    if (ok && wr && lane < 12) {
+        pre->q0[j] = X[j][12];
+        pre->t0[j] = t0;
+        pre->nsel[j] = s2;
+    }
+    lds_sync();  // X (aliasing L) is read completely before the factorisation writes L
+    return ok;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1163,11 +1318,23 @@ __device__ void update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
     }
     lds_sync();
     // the slot factorisation of the solve's start, here where the robot's own contact mask is
-    // known (not under mode hypotheses, whose masks differ per QP): in the update kernel four
-    // robots share a wave, so this 12-lane work costs a quarter of its one-robot-per-wave price
+    // known: in the update kernel four robots share a wave, so this 12-lane work costs a quarter
+    // of its one-robot-per-wave price.  Four-contact stance eliminates its equalities first
+    // (stance_reduce) and factors the force-space Hessian instead.  Under mode hypotheses the
+    // masks differ per QP: the stance elimination is formed for every state (the bounds are
+    // written unmasked, i.e. as for stance legs, which is exactly the kappa = 15 hypothesis) and
+    // the other hypotheses factor their slot Hessian in the solve.
     if (pre) {
-        if (!a.modes) {
-            const bool ok = presolve<SUB>(P, kap, pr, lane, s.ps.L, s.ps.ild, s.ps.xs);
+        double hrow[12], gsv = 0.0;
+        bool stance = false;
+        if constexpr (SUB == 16) {
+            if (WBC_STANCE_ELIM && (kap == 15 || a.modes))
+                stance = stance_reduce(P, pr, lane, wr, s.ps.L, s.ps.ild, hrow, gsv, pre);
+        }
+        const bool fact = stance || !a.modes;
+        if (fact) {
+            if (!stance) slot_hessian_row(P, kap, pr, lane, hrow, gsv);
+            const bool ok = factor12<SUB>(hrow, gsv, lane, s.ps.L, s.ps.ild, s.ps.xs);
             const double (&Mi)[12][12] = *reinterpret_cast<const double(*)[12][12]>(&s.ps.L[0][0]);
             if (wr) {
                 for (int k = lane; k < 78; k += SUB) {
@@ -1175,11 +1342,13 @@ __device__ void update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
                     pre->Mi[k] = Mi[i][k - i * (i + 1) / 2];
                 }
                 if (lane < 12) pre->xs[lane] = s.ps.xs[lane];
-                if (lane == 0) pre->presolved = 1.0;
             }
-            if (lane == 0 && !ok) P.flags += 2.0;
-        } else if (lane == 0 && wr) {
-            pre->presolved = 0.0;
+            if (lane == 0 && !ok && !a.modes) P.flags += 2.0;
+            if (lane == 0 && !ok && stance) stance = false;  // modes: the kappa = 15 hypothesis factors H_s itself
+        }
+        if (lane == 0 && wr) {
+            pre->presolved = (fact && !stance) ? 1.0 : 0.0;
+            pre->stance = stance ? 1.0 : 0.0;
         }
         lds_sync();
     }
@@ -1317,29 +1486,32 @@ __device__ __forceinline__ void to_column(QpScratch& s, double* cc) {
 }
 
 // d = C[:, p] broadcast from lane p (uniform, v_readlane)
+template <int N>
 __device__ __forceinline__ void read_column(const double* cc, int p, double* d) {
 #pragma unroll
-    for (int k = 0; k < NQ; ++k) d[k] = WBC_LOOP_BPERM ? vbcast(cc[k], p) : bcast(cc[k], p);
+    for (int k = 0; k < N; ++k) d[k] = WBC_LOOP_BPERM ? vbcast(cc[k], p) : bcast(cc[k], p);
 }
-__device__ __forceinline__ void zero_rinv(QpScratch& s) {
+template <class S>
+__device__ __forceinline__ void zero_rinv(S& s) {
     double2* r = &s.Rv[0][0];
     const int lane = lane_id();
 #pragma unroll
-    for (int k = 0; k < (NQ / 2) * NQ; k += 64)
-        if (k + lane < (NQ / 2) * NQ) r[k + lane] = make_double2(0.0, 0.0);
+    for (int k = 0; k < (S::N / 2) * S::N; k += 64)
+        if (k + lane < (S::N / 2) * S::N) r[k + lane] = make_double2(0.0, 0.0);
 }
 // r = R^-1 d (lane i < q holds r_i; rows >= q and columns >= q of R^-1 are zero)
-__device__ __forceinline__ double rinv_times_d(const QpScratch& s, const double* d) {
+template <class S>
+__device__ __forceinline__ double rinv_times_d(const S& s, const double* d) {
     const int lane = lane_id();
-    const int i = lane < NQ ? lane : 0;
+    const int i = lane < S::N ? lane : 0;
     double acc[4] = {0.0, 0.0, 0.0, 0.0};  // independent chains
 #pragma unroll
-    for (int jj = 0; jj < NQ / 2; ++jj) {
+    for (int jj = 0; jj < S::N / 2; ++jj) {
         const double2 v = s.Rv[jj][i];
         acc[(2 * jj) & 3] += v.x * d[2 * jj];
         acc[(2 * jj + 1) & 3] += v.y * d[2 * jj + 1];
     }
-    return lane < NQ ? (acc[0] + acc[1]) + (acc[2] + acc[3]) : 0.0;
+    return lane < S::N ? (acc[0] + acc[1]) + (acc[2] + acc[3]) : 0.0;
 }
 // add the constraint with column d at position q: Householder on rows q..23 of every C column
 // (v = d with rows < q zeroed on entry, the Householder vector on exit; dq = d[q]); R^-1 gains the column [-r / alpha; 1 / alpha]
@@ -1361,14 +1533,16 @@ __device__ __forceinline__ double householder(int q, bool add, double zn, double
     for (int k = 0; k < NQ; ++k) cc[k] -= vw * v[k];
     return ia;
 }
-__device__ __forceinline__ void store_rinv_column(QpScratch& s, int q, bool add, double ia, double rk) {
+template <class S>
+__device__ __forceinline__ void store_rinv_column(S& s, int q, bool add, double ia, double rk) {
     const int lane = lane_id();
     if (add && lane <= q) {
         double* col = reinterpret_cast<double*>(&s.Rv[q >> 1][lane]) + (q & 1);
         *col = (lane == q) ? ia : -rk * ia;
     }
 }
-__device__ __forceinline__ void add_column(QpScratch& s, int q, bool add, double zn, double dq, double rk,
+template <class S>
+__device__ __forceinline__ void add_column(S& s, int q, bool add, double zn, double dq, double rk,
                                            double* v, double* cc) {
     store_rinv_column(s, q, add, householder(q, add, zn, dq, v, cc), rk);
 }
@@ -1376,6 +1550,7 @@ __device__ __forceinline__ void add_column(QpScratch& s, int q, bool add, double
 // c -= vw v is c -= vw d2 plus vw alpha at row q.  d2 (the column masked to rows >= q), cz = c^T d2
 // and cq = c[q] come in precomputed with fp64 0 / 1 row masks (one multiply or FMA per row instead
 // of a two-instruction v_cndmask select per row for every dynamic-position insert and extract).
+template <int N>
 __device__ __forceinline__ double householder_masked(int q, bool add, double zn, double dq, double cz, double cq,
                                                      const double* d2, double* cc) {
     if (!add) { zn = 1.0; dq = 0.0; }
@@ -1387,7 +1562,7 @@ __device__ __forceinline__ double householder_masked(int q, bool add, double zn,
     const double vw = add ? (cz - alpha * cq) * beta : 0.0;
     const double vwa = vw * alpha;
 #pragma unroll
-    for (int k = 0; k < NQ; ++k) {
+    for (int k = 0; k < N; ++k) {
         const double ok = (k == q) ? 1.0 : 0.0;
         cc[k] = fma(vwa, ok, fma(-vw, d2[k], cc[k]));
     }
@@ -1401,18 +1576,19 @@ __device__ __forceinline__ double householder_masked(int q, bool add, double zn,
 // columns of R^-1, and the new R^-1 is R^-1 G^T without row l and column q (rows of the old inverse
 // shift up by one).  Row and column loops are unrolled with wave-uniform guards, so every register
 // index is static.
-__device__ void givens_drop(QpScratch& s, int l, int q, int act, double* cc) {
+template <class S>
+__device__ void givens_drop(S& s, int l, int q, int act, double* cc) {
     const int lane = lane_id();
-    const int i = lane < NQ ? lane : 0;
-    double rr[NQ];  // row i of R^-1
+    const int i = lane < S::N ? lane : 0;
+    double rr[S::N];  // row i of R^-1
 #pragma unroll
-    for (int jj = 0; jj < NQ / 2; ++jj) {
+    for (int jj = 0; jj < S::N / 2; ++jj) {
         const double2 v = s.Rv[jj][i];
         rr[2 * jj] = v.x;
         rr[2 * jj + 1] = v.y;
     }
 #pragma unroll
-    for (int k = 0; k < NQ - 1; ++k) {
+    for (int k = 0; k < S::N - 1; ++k) {
         if (k >= l && k < q) {
             const int pl = bcast_i(act, k);
             const double a0 = bcast(cc[k], pl), b0 = bcast(cc[k + 1], pl);
@@ -1430,13 +1606,13 @@ __device__ void givens_drop(QpScratch& s, int l, int q, int act, double* cc) {
     // rows >= l take the next row; the triangle below the diagonal, row >= q and column >= q are 0
     const int src = lane + ((lane >= l) ? 1 : 0);
 #pragma unroll
-    for (int k = 0; k < NQ; ++k) {
+    for (int k = 0; k < S::N; ++k) {
         const double v = __shfl(rr[k], src & 63);
         rr[k] = (lane < q && k >= lane && k < q) ? v : 0.0;
     }
-    if (lane < NQ) {
+    if (lane < S::N) {
 #pragma unroll
-        for (int jj = 0; jj < NQ / 2; ++jj) s.Rv[jj][lane] = make_double2(rr[2 * jj], rr[2 * jj + 1]);
+        for (int jj = 0; jj < S::N / 2; ++jj) s.Rv[jj][lane] = make_double2(rr[2 * jj], rr[2 * jj + 1]);
     }
 }
 
@@ -1444,12 +1620,13 @@ __device__ void givens_drop(QpScratch& s, int l, int q, int act, double* cc) {
 // act of slot lane) holds with equality, from the slacks sp0 at the unconstrained optimum x0:
 // R^T v = -s_A (v_i = -column i of R^-1 . s_A), u = R^-1 v, s = sp0 + C[0:q]^T v.  This is the state
 // the dual method reaches by adding those constraints with full steps (used by the hotstart).
-__device__ void active_set_point(const QpScratch& s, int q, int act, double sp0, const double* cc, double& u,
+template <class S>
+__device__ void active_set_point(const S& s, int q, int act, double sp0, const double* cc, double& u,
                                  double& sp) {
     const int lane = lane_id();
-    const int i = lane < NQ ? lane : 0;
+    const int i = lane < S::N ? lane : 0;
     double a4[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int j = 0; j < NQ; ++j) {
+    for (int j = 0; j < S::N; ++j) {
         if (j < q) {
             const int aj = bcast_i(act, j);
             const double sa = bcast(sp0, aj < 0 ? 0 : aj);
@@ -1459,7 +1636,7 @@ __device__ void active_set_point(const QpScratch& s, int q, int act, double sp0,
     }
     const double v = (lane < q) ? -((a4[0] + a4[1]) + (a4[2] + a4[3])) : 0.0;
     double u4[4] = {0.0, 0.0, 0.0, 0.0}, s4[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int j = 0; j < NQ; ++j) {
+    for (int j = 0; j < S::N; ++j) {
         if (j < q) {
             const double vj = bcast(v, j);
             const double2 r = s.Rv[j >> 1][i];  // R^-1 (i, j)
@@ -1846,7 +2023,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, const Pr
         IST(0);  // selection
         IST_COUNT(0);  // loop passes that reach the column broadcast (adds, drops, rebuild re-adds)
         double d[NQ];
-        read_column(cc, col, d);
+        read_column<NQ>(cc, col, d);
         IST(1);  // column broadcast
         const double rk = rinv_times_d(s, d);
         // d2 = rows >= pos of d, cq = this lane's c[pos] (fp64 0 / 1 row masks, uniform)
@@ -1911,7 +2088,7 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, const Pr
         }
         IST(3);  // step length, multipliers
         // one in-place update site for every path (no second live copy of cc)
-        store_rinv_column(s, pos, add, householder_masked(pos, add, zn, dq, cz, cq, d, cc), rk);
+        store_rinv_column(s, pos, add, householder_masked<NQ>(pos, add, zn, dq, cz, cq, d, cc), rk);
         IST(4);  // Householder update
         if (add) {
             if (rebuild) {
@@ -2037,6 +2214,351 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, const Pr
     }
 }
 
+constexpr int PRE_STANCE = 91;  // packed index of Presolve::stance
+static_assert(offsetof(Presolve, stance) == PRE_STANCE * sizeof(double), "PRE_STANCE");
+static_assert(offsetof(Presolve, t0) == 104 * sizeof(double) && offsetof(Presolve, nsel) == 116 * sizeof(double),
+              "Presolve stance packing (t0 / nsel in PreRegs::v1 lanes 40.. / 52..)");
+
+// solveQP + computeJointTorques (cpp:466-577) for a four-contact stance robot whose equalities
+// the update kernel eliminated (stance_reduce): Goldfarb-Idnani on the 12 contact forces with the
+// 40 inequality rows, one per lane.  Lane p holds constraint 12 + p of the general numbering
+// (friction faces 12..27, torque rows 28..51; the 12 equalities hold by construction), so the
+// selection order, the reference-space row scales and the hotstart working-set bits are the
+// general path's.  The dual iterates are those of the general solve after its equality block
+// (same QP restricted to the equality manifold), which the iteration-parity tests check.
+//   friction face rr of leg l:  -D_rr f_l >= 0                       (cpp:404-424)
+//   torque row j, sign sg:      sg (t0_j - Nt_j f) >= -tau_max       (cpp:495,506,513)
+__device__ void solve_stance(const KernelArgs& a, int rb, const Prob& P, const PreRegs& pf, const Presolve* rec,
+                             StanceScratch& s) {
+    constexpr int N = StanceScratch::N, MC = StanceScratch::MC, NEQ = 12;
+    const wbc_params& pr = *a.params;
+    const int lane = lane_id();
+    int status = (P.flags != 0.0) ? WBC_QP_NUMERIC : WBC_QP_OK;
+    int iters = 0;
+    // M (packed p < 78: M(i, j), p = i (i + 1) / 2 + j) and f0 (78..89) from the record registers
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int p = lane + 64 * h;
+        const double v = h ? pf.v1 : pf.v0;
+        if (p < 78) {
+            const int i = (int)((sqrt(8.0 * p + 1.0) - 1.0) * 0.5);
+            s.Mi()[i][p - i * (i + 1) / 2] = v;
+        } else if (p < 90) {
+            s.xs[p - 78] = v;
+        }
+    }
+    for (int k = lane; k < 144; k += 64) {
+        const int i = k / 12, j = k % 12;
+        if (j > i) s.Mi()[i][j] = 0.0;
+    }
+    lds_sync();
+
+    // this lane's row: normal n (force space), bound b (n^T f >= b), reference-space scale
+    const bool is_con = lane < MC;
+    const bool fr = lane < 16, tq = lane >= 16 && lane < MC;
+    const int l = (lane >> 2) & 3, rr = lane & 3;
+    const int qt = tq ? lane - 16 : 0, k = qt >> 1;
+    const double sg = (qt & 1) ? -1.0 : 1.0;
+    double cc[N];
+    {
+        const double2* nt = reinterpret_cast<const double2*>(rec->Nt + k * 12);
+#pragma unroll
+        for (int j = 0; j < N; j += 2) {
+            const double2 v = nt[j / 2];
+            cc[j] = tq ? -sg * v.x : 0.0;
+            cc[j + 1] = tq ? -sg * v.y : 0.0;
+        }
+#pragma unroll
+        for (int mm = 0; mm < 4; ++mm) {
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                // friction face rr: (-1 | 1 | 0, 0 | 0 | -1 | 1, mu), as build_normal
+                const double fv = (r == 0) ? ((rr == 0) ? -1.0 : (rr == 1 ? 1.0 : 0.0))
+                                : (r == 1) ? ((rr == 2) ? -1.0 : (rr == 3 ? 1.0 : 0.0)) : pr.friction;
+                if (fr) cc[3 * mm + r] = (mm == l) ? fv : 0.0;
+            }
+        }
+    }
+    const double t0k = vbcast(pf.v1, 40 + k), nsk = vbcast(pf.v1, 52 + k);
+    const double bj = P.bbj[k];
+    const double bp = tq ? (-pr.max_torque - sg * t0k) : 0.0;
+    const double bref = tq ? (-pr.max_torque - sg * bj) : 0.0;  // the reference row's own bound
+    const double tolv = 1e-10 * fmax(1.0, fabs(bref));
+    const double inrm = 1.0 / sqrt(fmax(fr ? 1.0 + pr.friction * pr.friction : nsk, 1e-300));
+    double nn, sp;
+    {
+        double np[4] = {0.0, 0.0, 0.0, 0.0}, sq[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            np[j & 3] += cc[j] * cc[j];
+            sq[j & 3] += cc[j] * s.xs[j];
+        }
+        nn = (np[0] + np[1]) + (np[2] + np[3]);
+        sp = ((sq[0] + sq[1]) + (sq[2] + sq[3])) - bp;
+    }
+    {   // C0[:, p] = M n_p (M read as a broadcast)
+        double t[N];
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            double a4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int j = 0; j <= i; ++j) a4[j & 3] += s.Mi()[i][j] * cc[j];
+            t[i] = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+        }
+#pragma unroll
+        for (int i = 0; i < N; ++i) cc[i] = t[i];
+    }
+    const double sp0 = sp;
+    if (is_con) {
+#pragma unroll
+        for (int j = 0; j < N; j += 2) s.c0[j / 2][lane] = make_double2(cc[j], cc[j + 1]);
+    }
+    zero_rinv(s);
+    lds_sync();
+
+    int q = 0;         // active set size
+    double u = 0.0;    // multiplier of active slot `lane`
+    int act = -1;      // constraint (lane) of active slot `lane`
+    int pstar = -1;
+    int rbk = -1;      // rebuild cursor (hotstart re-adds)
+    double up = 0.0;
+    bool active = false;
+    const double tiny = 1e-26;
+    bool done = (status != WBC_QP_OK);
+
+    // hotstart (cpp:523-535): the previous working set, constraint ids 12.. -> lanes 0..
+    double* Hh = a.stateful ? a.hist + (size_t)rb * HIST_LEN : nullptr;
+    bool warm_fail = false;
+    if (!done && Hh && !a.cold) {
+        const unsigned long long ws = (unsigned long long)(unsigned)Hh[H_WSLO] |
+                                      ((unsigned long long)(unsigned)Hh[H_WSHI] << 32);
+        unsigned long long wm = ((int)Hh[H_WSKAP] == 15) ? (ws >> NEQ) : 0ull;
+        wm &= (1ull << MC) - 1ull;
+        const int nw = __popcll(wm);
+        if (nw > 0 && nw <= N) {
+            const bool mine = (wm >> lane) & 1ull;
+            const int slot = __popcll(wm & ((1ull << lane) - 1ull));
+            if (mine) s.colbuf[slot] = (double)lane;
+            lds_sync();
+            if (lane < nw) act = (int)s.colbuf[lane];
+            if (mine) active = true;
+            lds_sync();
+            rbk = 0;
+            q = nw;
+        }
+    }
+    const int max_wsr = pr.max_wsr;
+
+    while (!done) {
+        asm volatile("" ::: "memory");
+        if (rbk >= q) {  // hotstart re-adds finished
+            rbk = -1;
+            active_set_point(s, q, act, sp0, cc, u, sp);
+            const bool neg = lane < q && u < -1e-10;
+            if (warm_fail || wave_any(neg)) {
+                // reject the warm set: cold start from the unconstrained optimum
+                if (is_con) {
+#pragma unroll
+                    for (int j = 0; j < N; j += 2) {
+                        const double2 c = s.c0[j / 2][lane];
+                        cc[j] = c.x;
+                        cc[j + 1] = c.y;
+                    }
+                }
+                zero_rinv(s);
+                lds_sync();
+                act = -1;
+                u = 0.0;
+                active = false;
+                q = 0;
+                sp = sp0;
+                continue;
+            }
+            if (lane < q && u < 0.0) u = 0.0;
+        }
+        const bool rebuild = rbk >= 0;
+        int col, pos;
+        if (rebuild) {
+            col = bcast_i(act, rbk);
+            pos = rbk;
+        } else {
+            if (pstar < 0) {  // most violated row, by slack / |reference row|
+                double v = 1e300;
+                if (is_con && !active && sp < -tolv) v = sp * inrm;
+                const int idx = wave_argmin_lane(v);
+                if (!(bcast(v, idx) < 1e299)) break;  // no violated constraint: optimal
+                pstar = idx;
+                up = 0.0;
+            }
+            if (++iters > max_wsr) { status = WBC_QP_MAX_ITER; iters = max_wsr; break; }
+            col = pstar;
+            pos = q;
+        }
+        double d[N];
+        read_column<N>(cc, col, d);
+        const double rk = rinv_times_d(s, d);
+        double czp[4] = {0.0, 0.0, 0.0, 0.0}, cqp[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            const double mk = (j >= pos) ? 1.0 : 0.0, ok = (j == pos) ? 1.0 : 0.0;
+            d[j] *= mk;
+            czp[j & 3] += cc[j] * d[j];
+            cqp[j & 3] += cc[j] * ok;
+        }
+        const double cz = (czp[0] + czp[1]) + (czp[2] + czp[3]);
+        const double cq = (cqp[0] + cqp[1]) + (cqp[2] + cqp[3]);
+        const double zn = bcast(cz, col);
+        const double dq = bcast(cq, col);
+
+        bool add = true, drop = false;
+        int drop_slot = -1;
+        if (rebuild && !(zn > tiny * fmax(1.0, bcast(nn, col)))) {
+            add = false;  // a warm row dependent on the others: reject the warm set
+            warm_fail = true;
+            ++rbk;
+        }
+        if (!rebuild) {
+            const double sps = bcast(sp, pstar);
+            double t1;
+            int l1;
+            {
+                double v = 1e300;
+                if (lane < q && rk > 1e-14) v = u * fast_rcp(rk);
+                l1 = wave_argmin_lane(v);
+                t1 = bcast(v, l1);
+            }
+            const double t2 = (zn > 1e-14) ? (-sps * fast_rcp(zn)) : 1e300;
+            const double t = fmin(t1, t2);
+            if (!(t < 1e299)) { status = WBC_QP_INFEASIBLE; break; }
+            const bool full = (t2 < 1e299 && t2 <= t1);
+            if (t2 < 1e299) sp += t * cz;
+            if (lane < q) u -= t * rk;
+            up += t;
+            if (!full) {
+                add = false;
+                drop = true;
+                drop_slot = l1;
+                const int dropped = bcast_i(act, l1);
+                if (lane == dropped) active = false;
+                const double un = __shfl(u, (lane + 1) & 63);
+                const int an = __shfl(act, (lane + 1) & 63);
+                if (lane >= l1 && lane < q - 1) { u = un; act = an; }
+                if (lane == q - 1) { u = 0.0; act = -1; }
+                --q;
+            }
+        }
+        store_rinv_column(s, pos, add, householder_masked<N>(pos, add, zn, dq, cz, cq, d, cc), rk);
+        if (add) {
+            if (rebuild) {
+                ++rbk;
+            } else {
+                if (lane == q) { u = up; act = pstar; }
+                if (lane == pstar) active = true;
+                ++q;
+                pstar = -1;
+            }
+            lds_sync();
+        }
+        if (drop) {
+            givens_drop(s, drop_slot, q, act, cc);
+            lds_sync();
+        }
+    }
+
+    // primal: f = f0 + H_f^-1 N_A u = f0 + M^T w',  w' = sum_s u_s C0[:, a_s]
+    double wi;
+    {
+        const int i = lane < N ? lane : 0;
+        double w4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k0 = 0; k0 < N; k0 += 4) {
+            if (k0 < q) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int ak = bcast_i(act, k0 + j);
+                    const double2 c = s.c0[i >> 1][ak < 0 ? 0 : ak];
+                    w4[j] = fma(bcast(u, k0 + j), (i & 1) ? c.y : c.x, w4[j]);
+                }
+            }
+        }
+        wi = (w4[0] + w4[1]) + (w4[2] + w4[3]);
+    }
+    {
+        const int i = lane < N ? lane : 0;
+        double x4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k2 = 0; k2 < N; ++k2) x4[k2 & 3] += s.Mi()[k2][i] * bcast(wi, k2);
+        if (lane < N) s.ucon[lane] = s.xs[i] + ((x4[0] + x4[1]) + (x4[2] + x4[3]));
+    }
+    lds_sync();
+    const bool ok = (status == WBC_QP_OK);
+    // torques tau_j = t0_j - Nt_j f (cpp:565-576), grf = f (cpp:556-563), qdd = q0 - P f
+    const double t0j = vbcast(pf.v1, 40 + (lane < 12 ? lane : 0));  // all lanes: ds_bpermute reads 0 from inactive ones
+    if (lane < 12) {
+        const int j = lane;
+        const double2* nt = reinterpret_cast<const double2*>(rec->Nt + j * 12);
+        const double2* pp = reinterpret_cast<const double2*>(rec->P + j * 12);
+        double t4[4] = {0.0, 0.0, 0.0, 0.0}, q4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int c = 0; c < 12; c += 2) {
+            const double2 nv = nt[c / 2];
+            t4[c & 3] = fma(nv.x, s.ucon[c], t4[c & 3]);
+            t4[(c + 1) & 3] = fma(nv.y, s.ucon[c + 1], t4[(c + 1) & 3]);
+            if (a.x) {
+                const double2 pv = pp[c / 2];
+                q4[c & 3] = fma(pv.x, s.ucon[c], q4[c & 3]);
+                q4[(c + 1) & 3] = fma(pv.y, s.ucon[c + 1], q4[(c + 1) & 3]);
+            }
+        }
+        const double tv = t0j - ((t4[0] + t4[1]) + (t4[2] + t4[3]));
+        a.tau[(size_t)rb * 12 + lane] = ok ? tv : 0.0;
+        a.grf[(size_t)rb * 12 + lane] = ok ? s.ucon[j] : 0.0;
+        if (a.x) s.ucon[12 + j] = rec->q0[j] - ((q4[0] + q4[1]) + (q4[2] + q4[3]));
+    }
+    if (a.x) {
+        lds_sync();
+        if (lane < 42) {
+            double xv;
+            if (lane < 6) {  // a = Mbar_b^-1 (Jc_com^T f - gw)
+                double F[3] = {0, 0, 0}, Mm[3] = {0, 0, 0};
+#pragma unroll
+                for (int ll = 0; ll < 4; ++ll) {
+                    const double fl[3] = {s.ucon[3 * ll], s.ucon[3 * ll + 1], s.ucon[3 * ll + 2]};
+                    const double dl[3] = {P.d[3 * ll], P.d[3 * ll + 1], P.d[3 * ll + 2]};
+                    double t[3];
+                    cross3(dl, fl, t);
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) { F[i] += fl[i]; Mm[i] += t[i]; }
+                }
+                if (lane < 3) xv = sel3(F, lane) * P.inv_m - (lane == 2 ? pr.gravity : 0.0);
+                else {
+                    const int r3 = lane - 3;
+                    xv = P.Icinv[3 * r3] * Mm[0] + P.Icinv[3 * r3 + 1] * Mm[1] + P.Icinv[3 * r3 + 2] * Mm[2];
+                }
+            } else if (lane < 18) {
+                xv = s.ucon[12 + lane - 6];
+            } else if (lane < 30) {
+                xv = s.ucon[lane - 18];
+            } else {
+                xv = fabs(P.rsw[lane - 30]);
+            }
+            a.x[(size_t)rb * WBC_NV + lane] = ok ? xv : 0.0;
+        }
+    }
+    if (lane == 0) {
+        a.status[rb] = status;
+        a.iters[rb] = iters;
+    }
+    if (Hh) {  // working set for the next cycle's hotstart, in the general numbering
+        const unsigned long long am = __ballot(is_con && active) << NEQ;
+        if (lane == 0) {
+            Hh[H_WSLO] = ok ? (double)(unsigned)(am & 0xffffffffull) : 0.0;
+            Hh[H_WSHI] = ok ? (double)(unsigned)(am >> 32) : 0.0;
+            Hh[H_WSKAP] = 15.0;
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // kernels: one 64-lane workgroup per robot
 // ---------------------------------------------------------------------------------------
@@ -2069,7 +2591,10 @@ struct UpdLds {
 };
 struct SolveLds {
     Prob prob;
-    QpScratch q;
+    union {
+        QpScratch q;
+        StanceScratch st;
+    };
 };
 
 WBC_KERNEL_ATTR void wbc_step_kernel(KernelArgs a) {
@@ -2137,7 +2662,10 @@ WBC_KERNEL_ATTR void wbc_solve_kernel(KernelArgs a) {
         if (lane == 0) L.prob.kappa = (double)kap;
     }
     wsync();
-    solve_phase(a, rb, L.prob, &pf, L.q);
+    if (WBC_STANCE_ELIM && (int)L.prob.kappa == 15 && bcast(pf.v1, PRE_STANCE - 64) != 0.0)
+        solve_stance(a, rb, L.prob, pf, reinterpret_cast<const Presolve*>(prow), L.st);
+    else
+        solve_phase(a, rb, L.prob, &pf, L.q);
 }
 
 __global__ void wbc_reset_kernel(double* hist, const uint8_t* mask, int batch) {

@@ -48,11 +48,23 @@ constexpr int PROB_LEN = sizeof(Prob) / sizeof(double);
 
 // Slot factorisation formed at the end of the update kernel (presolve in wbc_kernel.hip), stored
 // after the problem in the work row and read by the solve kernel from HBM / L2.
+//
+// Four-contact stance (kappa = 15) is solved in a smaller space: the 12 stance equalities
+// (R1, cpp:494,504) Jbar_c,j qdd + G f = e are solved for qdd = q0 - P f (Gauss-Jordan with
+// partial pivoting in the update kernel), which leaves a 12-variable QP in the contact forces
+// with Hessian H_f = P^T P + H_s and gradient g_s - P^T q0, and only inequality rows
+// (16 friction faces, 24 torque rows tau = t0 - Nt f).  Then Mi / xs hold the factor of H_f and
+// the unconstrained f0, and the stance fields below are filled.
 struct Presolve {
-    double Mi[78];    // M = L^-1 of the slot Hessian H_s = L L^T, lower triangle row-major
-    double xs[12];    // slot part of the unconstrained optimum x0 = -H^-1 g
-    double presolved; // 1: Mi / xs hold the factorisation for this kappa; 0: the solve forms it
-    double pad_;
+    double Mi[78];    // M = L^-1 of the slot Hessian H_s = L L^T (H_f for stance), lower triangle row-major
+    double xs[12];    // slot part of the unconstrained optimum x0 = -H^-1 g (f0 for stance)
+    double presolved; // 1: Mi / xs hold the slot factorisation for this kappa; 0: the solve forms it
+    double stance;    // 1: the stance elimination below is valid (Mi / xs then belong to H_f)
+    double q0[12];    // stance: qdd = q0 - P f
+    double t0[12];    //         tau = t0 - Nt f  (t0 = bbar_j + Mbar_j q0)
+    double nsel[12];  //         |row|^2 of torque row j in the reference's 42-variable space
+    double Nt[144];   //         Nt = Mbar_j P + Jbar_c,j^T, [joint j][force c]
+    double P[144];    //         P = Jbar_c,j^-1 G, [joint][force]
 };
 static_assert(sizeof(Presolve) % 16 == 0, "Presolve must keep 16-byte alignment");
 constexpr int PRE_LEN = sizeof(Presolve) / sizeof(double);

@@ -94,6 +94,16 @@ def test_update_solve_split_equals_fused():
     e.step(STATELESS | SPLIT)  # update kernel + solve kernel
     step = e.outputs()
     e.close()
+    # four-contact stance rows take the force-space solve in the split form (equalities eliminated
+    # in the update kernel) and the 24-variable solve in the fused kernel: same QP, same working
+    # sets, agreement to rounding; every other row runs the same code in both forms: bitwise
+    st = inp["contacts"] == 15
+    assert st.any() and (~st).any()
     for k in ("tau", "grf", "x", "status", "iters"):
-        assert np.array_equal(fused[k], split[k]), k
+        assert np.array_equal(fused[k][~st], split[k][~st]), k
         assert np.array_equal(step[k], split[k]), k
+    assert np.array_equal(fused["status"][st], split["status"][st])
+    assert np.array_equal(fused["iters"][st], split["iters"][st])
+    for k, tol in (("tau", 1e-9), ("grf", 1e-9), ("x", 1e-8)):
+        scale = 1.0 + np.abs(fused[k][st]).max()
+        assert np.abs(fused[k][st] - split[k][st]).max() <= tol * scale, k
