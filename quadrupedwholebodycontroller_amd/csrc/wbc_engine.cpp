@@ -15,9 +15,11 @@
 
 extern "C" hipError_t wbc_launch_step(const wbc::KernelArgs* a, hipStream_t st);
 extern "C" hipError_t wbc_launch_update(const wbc::KernelArgs* a, hipStream_t st);
-extern "C" hipError_t wbc_launch_solve(const wbc::KernelArgs* a, hipStream_t st);
+extern "C" hipError_t wbc_launch_solve_general(const wbc::KernelArgs* a, hipStream_t st);
+extern "C" hipError_t wbc_launch_solve_stance(const wbc::KernelArgs* a, hipStream_t st);
 extern "C" int wbc_kernel_default_split();
 extern "C" hipError_t wbc_launch_reset(double* hist, const uint8_t* mask, int batch, hipStream_t st);
+extern "C" int wbc_kernel_stance_elim();
 
 namespace {
 thread_local std::string g_err;
@@ -66,6 +68,15 @@ struct wbc_engine {
     // state / outputs
     double* d_hist = nullptr;
     double* d_work = nullptr;
+    int32_t* d_fb = nullptr;  // elimination fallback counters [2] + list [B] (KernelArgs::fb)
+    int32_t parity = 0;       // fallback counter of the next update
+    // four-contact rows among the engine's own contact masks (d_contacts, as last copied from the
+    // host) and among the mode masks: the stance elimination runs when every QP of a step has
+    // mask 15 (known only for the engine's own masks; device-bound masks take the general path)
+    int64_t n_stance_own = 0;
+    int32_t modes_stance = 0;
+    bool elim = false;        // the last update's choice (its solve follows it)
+    int32_t elim_parity = 0;  // and its fallback counter
     double* d_tau = nullptr;
     double* d_grf = nullptr;
     double* d_x = nullptr;
@@ -125,7 +136,36 @@ wbc::KernelArgs make_args(wbc_engine* h, uint32_t flags) {
     a.cold = (flags & WBC_COLD) ? 1 : 0;
     a.modes = 0;
     a.mode_masks = h->d_modes;
+    a.elim = 0;
+    a.parity = 0;
+    a.fb = h->d_fb;
     return a;
+}
+
+int64_t count_stance(const uint8_t* masks, size_t n) {
+    int64_t c = 0;
+    for (size_t i = 0; i < n; ++i) c += (masks[i] & 15) == 15;
+    return c;
+}
+
+// Stance elimination for this update: on when every QP has mask 15 (a mixed batch would pay the
+// elimination in the update kernel's mixed waves and a second solve kernel's latency; measured
+// slower, profiles/r02/k), which the host knows for its own contact masks and for mode masks.
+void begin_update(wbc_engine* h, wbc::KernelArgs& a) {
+    bool all = false;
+    if (h->n_modes) all = h->modes_stance == h->n_modes;
+    else if (h->in_contacts == h->d_contacts) all = h->n_stance_own == h->batch;
+    h->elim = all && wbc_kernel_stance_elim();
+    h->elim_parity = h->parity;
+    h->parity ^= 1;
+    a.elim = h->elim ? 1 : 0;
+    a.parity = h->elim_parity;
+}
+
+hipError_t launch_solves(wbc_engine* h, wbc::KernelArgs& a) {
+    a.elim = h->elim ? 1 : 0;
+    a.parity = h->elim_parity;
+    return h->elim ? wbc_launch_solve_stance(&a, h->stream) : wbc_launch_solve_general(&a, h->stream);
 }
 }  // namespace
 
@@ -207,6 +247,7 @@ int32_t wbc_create(const wbc_model* model, const wbc_params* params, int32_t bat
     ALLOC(d_modes, WBC_MAX_MODES);
     ALLOC(d_hist, B * wbc::HIST_LEN);
     ALLOC(d_work, B * wbc::WORK_LEN);
+    ALLOC(d_fb, 2 + B);
     ALLOC(d_dbg, B * WBC_DBG_LEN);
 #undef ALLOC
     if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess ||
@@ -215,6 +256,7 @@ int32_t wbc_create(const wbc_model* model, const wbc_params* params, int32_t bat
         return fail(WBC_ERR_HIP, "stream/event creation failed");
     }
     h->stream = h->own_stream;
+    h->n_stance_own = B;  // d_contacts starts as all-stance (15), below
     h->in_pose = h->d_pose;
     h->in_nu = h->d_nu;
     h->in_qj = h->d_qj;
@@ -241,6 +283,7 @@ int32_t wbc_create(const wbc_model* model, const wbc_params* params, int32_t bat
         hipMemsetAsync(h->d_grf, 0, B * WBC_NUM_JOINTS * sizeof(double), st) != hipSuccess ||
         hipMemsetAsync(h->d_x, 0, B * WBC_NV * sizeof(double), st) != hipSuccess ||
         hipMemsetAsync(h->d_dbg, 0, B * WBC_DBG_LEN * sizeof(double), st) != hipSuccess ||
+        hipMemsetAsync(h->d_fb, 0, (2 + B) * sizeof(int32_t), st) != hipSuccess ||
         wbc_launch_reset(h->d_hist, nullptr, batch, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
         wbc_destroy(h);
         return fail(WBC_ERR_HIP, "wbc_create: initialisation failed");
@@ -256,7 +299,7 @@ int32_t wbc_destroy(wbc_engine* h) {
     // stream that was already destroyed
     (void)hipDeviceSynchronize();
     void* ptrs[] = {h->d_model, h->d_params, h->d_inblk, h->d_outblk, h->d_mask, h->d_modes, h->d_hist, h->d_work,
-                    h->d_dbg};
+                    h->d_fb, h->d_dbg};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (h->h_in) (void)hipHostFree(h->h_in);
@@ -299,7 +342,11 @@ int32_t wbc_set_reference(wbc_engine* h, const double* ref, const uint8_t* conta
     WBC_HIP(hipSetDevice(h->device));
     const size_t B = input_rows(h);
     if (ref) { WBC_HIP(hipMemcpyAsync(h->d_ref, ref, B * WBC_REF_LEN * sizeof(double), hipMemcpyHostToDevice, h->stream)); h->in_ref = h->d_ref; }
-    if (contacts) { WBC_HIP(hipMemcpyAsync(h->d_contacts, contacts, B, hipMemcpyHostToDevice, h->stream)); h->in_contacts = h->d_contacts; }
+    if (contacts) {
+        WBC_HIP(hipMemcpyAsync(h->d_contacts, contacts, B, hipMemcpyHostToDevice, h->stream));
+        h->in_contacts = h->d_contacts;
+        h->n_stance_own = count_stance(contacts, B);
+    }
     if (switching) { WBC_HIP(hipMemcpyAsync(h->d_switching, switching, B, hipMemcpyHostToDevice, h->stream)); h->in_switching = h->d_switching; }
     WBC_HIP(hipStreamSynchronize(h->stream));
     return WBC_OK;
@@ -347,6 +394,7 @@ int32_t wbc_update(wbc_engine* h, uint32_t flags) {
     if (h->n_modes) return fail(WBC_ERR_STATE, "wbc_update: mode hypotheses are set (use wbc_step_modes, or wbc_set_modes(h, 0, NULL))");
     WBC_HIP(hipSetDevice(h->device));
     wbc::KernelArgs a = make_args(h, flags);
+    begin_update(h, a);
     WBC_HIP(wbc_launch_update(&a, h->stream));
     h->updated = true;
     return WBC_OK;
@@ -358,7 +406,7 @@ int32_t wbc_solve(wbc_engine* h, uint32_t flags) {
     if (!h->updated) return fail(WBC_ERR_STATE, "wbc_solve before wbc_update");
     WBC_HIP(hipSetDevice(h->device));
     wbc::KernelArgs a = make_args(h, flags);
-    WBC_HIP(wbc_launch_solve(&a, h->stream));
+    WBC_HIP(launch_solves(h, a));
     return WBC_OK;  // the assembled problem stays valid: solving it again gives the same result
 }
 
@@ -372,8 +420,9 @@ int32_t wbc_step(wbc_engine* h, uint32_t flags) {
     // default form chosen at build time (WBC_DEFAULT_SPLIT, by measurement); the flags force one
     const bool split = (flags & WBC_SPLIT) || (!(flags & WBC_FUSED) && wbc_kernel_default_split());
     if (split) {
+        begin_update(h, a);
         WBC_HIP(wbc_launch_update(&a, h->stream));
-        WBC_HIP(wbc_launch_solve(&a, h->stream));
+        WBC_HIP(launch_solves(h, a));
     } else {
         WBC_HIP(wbc_launch_step(&a, h->stream));
     }
@@ -399,6 +448,7 @@ int32_t wbc_set_modes(wbc_engine* h, int32_t n_modes, const uint8_t* modes) {
     WBC_HIP(hipMemcpyAsync(h->d_modes, modes, (size_t)n_modes, hipMemcpyHostToDevice, h->stream));
     WBC_HIP(hipStreamSynchronize(h->stream));
     h->n_modes = n_modes;
+    h->modes_stance = (int32_t)count_stance(modes, (size_t)n_modes);
     return WBC_OK;
 }
 
@@ -410,12 +460,13 @@ int32_t wbc_step_modes(wbc_engine* h, uint32_t flags) {
     WBC_HIP(hipSetDevice(h->device));
     wbc::KernelArgs a = make_args(h, flags);
     a.modes = h->n_modes;
+    begin_update(h, a);
     const bool timed = (flags & WBC_TIMED) != 0;
     if (timed) WBC_HIP(hipEventRecord(h->ev0, h->stream));
     wbc::KernelArgs au = a;  // the update runs once per state
     au.batch = h->batch / h->n_modes;
     WBC_HIP(wbc_launch_update(&au, h->stream));
-    WBC_HIP(wbc_launch_solve(&a, h->stream));
+    WBC_HIP(launch_solves(h, a));
     if (timed) {
         WBC_HIP(hipEventRecord(h->ev1, h->stream));
         h->timed = true;
@@ -448,6 +499,7 @@ int32_t wbc_cycle(wbc_engine* h, const double* base_pose, const double* nu, cons
     std::memcpy(hp, ref, B * WBC_REF_LEN * sizeof(double));
     hp += B * WBC_REF_LEN;
     std::memcpy(reinterpret_cast<uint8_t*>(hp), contacts, B);
+    h->n_stance_own = count_stance(contacts, B);
     std::memcpy(reinterpret_cast<uint8_t*>(hp) + B, switching, B);
     WBC_HIP(hipMemcpyAsync(h->d_inblk, h->h_in, inb, hipMemcpyHostToDevice, h->stream));
     // inputs from the engine's own block for this step only (caller bindings are restored after)

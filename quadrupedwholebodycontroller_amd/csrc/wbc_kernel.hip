@@ -58,6 +58,15 @@ struct UpdScratch {
             double ild[12];
             double xs[12];
         } ps;
+        struct {            // four-contact stance elimination (stance_reduce), before the factorisation
+            double W[12][6];    // rows of Jblk^-1 E
+            double w[12];       // Jblk^-1 e
+            double S[6][8];     // [I - K W | K w], then the rows of H^ = I + Mb^-2 + Mb^-1 Q Mb^-1
+            double Si[6][8];    // S^-1 (rows)
+            double Y[12][6];    // W S^-1
+            double q0[12];
+            double Q[6][8];     // [Y^T Y | Y^T q0]
+        } sr;
     };
     double ja[12][3];       // joint axis (world)
     double jo[12][3];       // joint origin (world)
@@ -309,6 +318,9 @@ __device__ __forceinline__ bool seg_any(bool p) {
 // Four-contact stance solved in the 12-variable force space (Presolve::stance, wbc_layout.h)
 #ifndef WBC_STANCE_ELIM
 #define WBC_STANCE_ELIM 1
+#endif
+#ifndef WBC_STANCE_KERNEL
+#define WBC_STANCE_KERNEL 1  // 1: stance QPs in wbc_solve_stance_kernel (+ fallback kernel); 0: in wbc_solve_kernel
 #endif
 __device__ __forceinline__ int xcd_robot() {
     if (!WBC_XCD_REMAP) return blockIdx.x;
@@ -596,113 +608,254 @@ __device__ __forceinline__ int seg16_argmax(double v) {
 }
 
 // Four-contact stance (kappa = 15): eliminate the 12 stance equalities Jbj qdd + G f = e (R1,
-// cpp:494,504; G = Jc_com Mbar_b^-1 Jc_com^T, e = r1 + g e_z) as qdd = q0 - P f by Gauss-Jordan
-// with partial pivoting on [Jbj | G | e] (row i in lane i), then form the force-space Hessian
-// row H_f = P^T P + H_s and gradient g_f = g_s - P^T q0 (returned in hrow / gsv for factor12),
-// the torque map Nt = Mbj P + Jbj^T, t0 = bbj + Mbj q0 and the torque rows' reference-space
-// norms; P, q0, Nt, t0 and nsel go straight to the Presolve record.  X aliases the factor's L
-// area (its lifetime ends before the factorisation), piv the ild / xs area.  Returns false
-// (nothing stored; the caller takes the general path) when a pivot is below 1e-9 of the largest
-// entry of Jbj.  SUB = 16 only (one robot per DPP row).
-__device__ bool stance_reduce(const Prob& P, const wbc_params& pr, int lane, bool wr, double (&X)[12][13],
-                              double* piv, double (&hrow)[12], double& gsv, Presolve* pre) {
-    const int i = lane < 12 ? lane : 11;
-    double a[12], rhs[13];
+// cpp:494,504; G = E Mb^-1 E^T with E = Jc_com, rows [I, -S(d_l)]; e = r1 + g e_z) as qdd = q0 - P f.
+// Jbj = Jblk - E K is the block-diagonal foot Jacobian (one 3x3 block per leg) minus a rank-6 term
+// (K = Mb^-1 A_j), so by Woodbury, with W = Jblk^-1 E and S = I6 - K W:
+//   Jbj^-1 E = W S^-1 = Y,   q0 = Jbj^-1 e = w + Y K w (w = Jblk^-1 e),   P = Y Mb^-1 E^T,
+// and the force-space Hessian H_f = H_s + P^T P = I + E H^ E^T with H^ = I + Mb^-2 + Mb^-1 Y^T Y Mb^-1
+// (H_s = I + E (I + Mb^-2) E^T).  Per robot that is four 3x3 inverses, one 6x6 inverse and a few
+// 12 x 6 products; no 12-step elimination chain.  Also formed: the gradient g_f = g_s - P^T q0,
+// the torque map Nt = Mbj P + Jbj^T and t0 = bbj + Mbj q0 (stored with Y, q0 and the torque
+// rows' reference-space norms), H_f row i and g_f in hrow / gsv for factor12.  Returns false
+// (nothing usable stored; the caller takes the general path) at a near-singular leg or S.
+// Lane i < 12 of the segment is row i = 3 l + k; SUB = 16 only (one robot per DPP row).
+__device__ bool stance_reduce([[maybe_unused]] const KernelArgs& ka, [[maybe_unused]] int rb, const Prob& P,
+                              const wbc_params& pr, int lane, bool wr, UpdScratch& s, double (&hrow)[12],
+                              double& gsv, Presolve* pre) {
+    auto& R = s.sr;
+    const int i = lane < 12 ? lane : 11, l = i / 3, k = i % 3;
+    const double dl[3] = {P.d[3 * l], P.d[3 * l + 1], P.d[3 * l + 2]};
+    const double inv_m = P.inv_m;
+    // row k of Jblk_l^-1 and the leg's conditioning
+    double jr[3];
+    bool ok;
+    {
+        const double* A = s.Jf[l];
+        const double c00 = A[4] * A[8] - A[5] * A[7], c01 = A[5] * A[6] - A[3] * A[8], c02 = A[3] * A[7] - A[4] * A[6];
+        const double det = A[0] * c00 + A[1] * c01 + A[2] * c02;
+        double amx = 0.0;
 #pragma unroll
-    for (int j = 0; j < 12; ++j) a[j] = P.Jbj[i * 12 + j];
-    g_row(P, i, rhs);
-    rhs[12] = P.r1[i] + ((i % 3) == 2 ? pr.gravity : 0.0);
-    double amax = 0.0;
+        for (int t = 0; t < 9; ++t) amx = fmax(amx, fabs(A[t]));
+        ok = fabs(det) > 1e-9 * amx * amx * amx;
+        const double id = fast_rcp(ok ? det : 1.0);
+        const double r0[3] = {c00, A[2] * A[7] - A[1] * A[8], A[1] * A[5] - A[2] * A[4]};
+        const double r1[3] = {c01, A[0] * A[8] - A[2] * A[6], A[2] * A[3] - A[0] * A[5]};
+        const double r2[3] = {c02, A[1] * A[6] - A[0] * A[7], A[0] * A[4] - A[1] * A[3]};
 #pragma unroll
-    for (int j = 0; j < 12; ++j) amax = fmax(amax, fabs(a[j]));
-    bool pivoted = lane >= 12;
-    int my_step = 0;
-    double min_piv = 1e300;
-#pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        const int p = seg16_argmax(pivoted ? 0.0 : fabs(a[k]));
-        if (lane == p) {
-            // pivot row: columns k+1..11 of the Jbj part at piv[c - 1], the 13 right-hand sides at 11..23
-#pragma unroll
-            for (int c = k + 1; c < 12; ++c) piv[c - 1] = a[c];
-#pragma unroll
-            for (int c = 0; c < 13; ++c) piv[11 + c] = rhs[c];
-            my_step = k;
-            pivoted = true;
-        }
-        const double pa = __shfl(a[k], ((int)threadIdx.x & ~15) + p);
-        lds_sync();
-        const double ip = 1.0 / pa;
-        min_piv = fmin(min_piv, fabs(pa));
-        const double fct = (lane == p) ? 0.0 : a[k] * ip;
-        const double own = (lane == p) ? ip : 1.0;
-#pragma unroll
-        for (int c = k + 1; c < 12; ++c) a[c] = fma(-fct, piv[c - 1], a[c] * own);
-#pragma unroll
-        for (int c = 0; c < 13; ++c) rhs[c] = fma(-fct, piv[11 + c], rhs[c] * own);
-        lds_sync();  // the next pivot row overwrites piv
+        for (int t = 0; t < 3; ++t) jr[t] = ((k == 0) ? r0[t] : (k == 1) ? r1[t] : r2[t]) * id;
     }
-    const double am = seg16_max(amax);
-    // min_piv is uniform over the segment; a pivot this small relative to the matrix means a leg
-    // at (or near) a singular configuration: the general path handles it
-    const bool ok = min_piv > 1e-9 * am;
-    // lane i holds row my_step of X = Jbj^-1 [G | e]: P (12) and q0
+    // W row i = [jr, d_l x jr], w_i = jr . e_l
     if (lane < 12) {
+        double dxj[3];
+        cross3(dl, jr, dxj);
+        double wi = 0.0;
 #pragma unroll
-        for (int c = 0; c < 13; ++c) X[my_step][c] = rhs[c];
+        for (int t = 0; t < 3; ++t) {
+            R.W[i][t] = jr[t];
+            R.W[i][3 + t] = dxj[t];
+            wi = fma(jr[t], P.r1[3 * l + t] + (t == 2 ? pr.gravity : 0.0), wi);
+        }
+        R.w[i] = wi;
     }
     lds_sync();
-    // lane j < 12: column j of P (H_f row j, g_f), row j of Nt (torque joint j); X and the
-    // problem are read from LDS inside the loops (few values live across them)
-    const int j = i;
-    slot_hessian_row(P, 15, pr, lane, hrow, gsv);
+    // [S | z] = [I - K W | K w], K[a][j] = A_j[a] / m (a < 3), (I_c^-1 A_ang)_j[a - 3]: 42 entries
+    for (int t = lane; t < 42; t += 16) {
+        const int ra = t / 7, cb = t % 7;
+        double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+            const double kj = (ra < 3) ? s.A[j][ra] * inv_m : s.KA[j][ra - 3];
+            acc[j & 3] = fma(kj, (cb < 6) ? R.W[j][cb] : R.w[j], acc[j & 3]);
+        }
+        const double v = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+        R.S[ra][cb] = (cb < 6) ? ((ra == cb ? 1.0 : 0.0) - v) : v;
+    }
+    lds_sync();
+    // S^-1 by Gauss-Jordan without pivoting (S is well conditioned: cond < 10 on the bench and
+    // stress states, smallest pivot > 0.25 max|S|; a pivot below 1e-6 max|S| takes the general
+    // path), row r in lane r < 6, pivot rows broadcast with DPP row_newbcast
     {
-        double pcol[12];
+        const int r = lane < 6 ? lane : 5;
+        double sr_[6], ir[6];
+        double smx = 0.0;
 #pragma unroll
-        for (int k = 0; k < 12; ++k) pcol[k] = X[k][j];
-        double gq[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int c = 0; c < 6; ++c) {
+            sr_[c] = R.S[r][c];
+            ir[c] = (r == c) ? 1.0 : 0.0;
+            smx = fmax(smx, fabs(R.S[c][0]));
+        }
 #pragma unroll
-        for (int k = 0; k < 12; ++k) gq[k & 3] = fma(pcol[k], X[k][12], gq[k & 3]);
-        gsv -= (gq[0] + gq[1]) + (gq[2] + gq[3]);
+        for (int c = 1; c < 6; ++c)
 #pragma unroll
-        for (int c = 0; c < 12; ++c) {
-            double h4[4] = {0.0, 0.0, 0.0, 0.0};
+            for (int rr = 0; rr < 6; ++rr) smx = fmax(smx, fabs(R.S[rr][c]));
+        double pmin = 1e300;
 #pragma unroll
-            for (int k = 0; k < 12; ++k) h4[k & 3] = fma(pcol[k], X[k][c], h4[k & 3]);
-            hrow[c] += (h4[0] + h4[1]) + (h4[2] + h4[3]);
+        for (int kk = 0; kk < 6; ++kk) {
+            const double pv = seg_bcast<16>(sr_[kk], kk);
+            pmin = fmin(pmin, fabs(pv));
+            const double ip = fast_rcp(pv);
+            double prow[12];
+#pragma unroll
+            for (int c = kk + 1; c < 6; ++c) prow[c] = seg_bcast<16>(sr_[c], kk);
+#pragma unroll
+            for (int c = 0; c <= kk; ++c) prow[6 + c] = seg_bcast<16>(ir[c], kk);
+            const double f = (lane == kk) ? 0.0 : sr_[kk] * ip;
+            const double own = (lane == kk) ? ip : 1.0;
+#pragma unroll
+            for (int c = kk + 1; c < 6; ++c) sr_[c] = fma(-f, prow[c], sr_[c] * own);
+#pragma unroll
+            for (int c = 0; c <= kk; ++c) ir[c] = fma(-f, prow[6 + c], ir[c] * own);
+        }
+        ok = ok && pmin > 1e-6 * smx;
+        UST(ka, rb, 12);  // leg inverses, S, S^-1
+        if (lane < 6) {
+#pragma unroll
+            for (int c = 0; c < 6; ++c) R.Si[lane][c] = ir[c];
         }
     }
-    // Nt row j = Mbj row j . P + Jbj column j; t0_j = bbj_j + Mbj row j . q0
-    double t4[4] = {0.0, 0.0, 0.0, 0.0}, s2 = 0.0;
+    ok = !seg_any<16>(!ok);  // every leg and S usable (uniform over the robot)
+    lds_sync();
+    // Y row i = W_i S^-1, q0_i = w_i + Y_i z
+    double yi[6];
+    {
+        double wrow[6];
 #pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        const double mk = P.Mbj[j * 12 + k], jc = P.Jbj[k * 12 + j];
-        t4[k & 3] = fma(mk, X[k][12], t4[k & 3]);
-        s2 = fma(mk, mk, fma(jc, jc, s2));
-    }
-    const double t0 = P.bbj[j] + ((t4[0] + t4[1]) + (t4[2] + t4[3]));
-#pragma unroll 1
-    for (int c = 0; c < 12; c += 2) {  // not unrolled: unrolled, the X reads of all columns are hoisted (spills)
-        double n0[4] = {0.0, 0.0, 0.0, 0.0}, n1[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int c = 0; c < 6; ++c) wrow[c] = R.W[i][c];
+        double q = R.w[i];
 #pragma unroll
-        for (int k = 0; k < 12; ++k) {
-            const double mk = P.Mbj[j * 12 + k];
-            n0[k & 3] = fma(mk, X[k][c], n0[k & 3]);
-            n1[k & 3] = fma(mk, X[k][c + 1], n1[k & 3]);
+        for (int c = 0; c < 6; ++c) {
+            double a4[2] = {0.0, 0.0};
+#pragma unroll
+            for (int t = 0; t < 6; ++t) a4[t & 1] = fma(wrow[t], R.Si[t][c], a4[t & 1]);
+            yi[c] = a4[0] + a4[1];
+            q = fma(yi[c], R.S[c][6], q);
         }
-        const double v0 = P.Jbj[c * 12 + j] + ((n0[0] + n0[1]) + (n0[2] + n0[3]));
-        const double v1 = P.Jbj[(c + 1) * 12 + j] + ((n1[0] + n1[1]) + (n1[2] + n1[3]));
+        if (lane < 12) {
+#pragma unroll
+            for (int c = 0; c < 6; ++c) R.Y[i][c] = yi[c];
+            R.q0[i] = q;
+        }
+    }
+    lds_sync();
+    // [Q | v] = [Y^T Y | Y^T q0]: 42 entries
+    for (int t = lane; t < 42; t += 16) {
+        const int ra = t / 7, cb = t % 7;
+        double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int j = 0; j < 12; ++j) acc[j & 3] = fma(R.Y[j][ra], (cb < 6) ? R.Y[j][cb] : R.q0[j], acc[j & 3]);
+        R.Q[ra][cb] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    }
+    lds_sync();
+    // H^ rows (lane a < 6) over S: H^ = I + Mb^-2 + Mb^-1 Q Mb^-1, Mb^-1 = diag(I / m, I_c^-1)
+    {
+        const int ra = lane < 6 ? lane : 5;
+        // T = Q Mb^-1, rows ra (lin) or 3..5 (ang, then I_c^-1 from the left)
+        auto qm = [&](int row, double* o) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) o[c] = R.Q[row][c] * inv_m;
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+                o[3 + c] = R.Q[row][3] * P.Icinv[c] + R.Q[row][4] * P.Icinv[3 + c] + R.Q[row][5] * P.Icinv[6 + c];
+        };
+        double hr[6];
+        if (ra < 3) {
+            qm(ra, hr);
+#pragma unroll
+            for (int c = 0; c < 6; ++c) hr[c] *= inv_m;
+            hr[ra] += 1.0 + inv_m * inv_m;
+        } else {
+            double t3[3][6];
+            qm(3, t3[0]); qm(4, t3[1]); qm(5, t3[2]);
+            const int a3 = ra - 3;
+            const double* ic = &P.Icinv[3 * a3];
+#pragma unroll
+            for (int c = 0; c < 6; ++c) hr[c] = ic[0] * t3[0][c] + ic[1] * t3[1][c] + ic[2] * t3[2][c];
+            hr[ra] += 1.0;
+#pragma unroll
+            for (int c = 0; c < 3; ++c)  // (I_c^-2)[a3][c]
+                hr[3 + c] += ic[0] * P.Icinv[c] + ic[1] * P.Icinv[3 + c] + ic[2] * P.Icinv[6 + c];
+        }
+        // v -> Mb^-1 v (uniform, every lane) for g_f
+        lds_sync();  // all reads of S's z column done
+        if (lane < 6) {
+#pragma unroll
+            for (int c = 0; c < 6; ++c) R.S[lane][c] = hr[c];
+        }
+    }
+    double uv[6];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) uv[c] = R.Q[c][6] * inv_m;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) uv[3 + c] = P.Icinv[3 * c] * R.Q[3][6] + P.Icinv[3 * c + 1] * R.Q[4][6] + P.Icinv[3 * c + 2] * R.Q[5][6];
+    lds_sync();
+    // H_f row i = e_i + E H^ E_i^T: h = H^ E_i^T, then E_j . h = h[k_j] - (d_{l_j} x h_ang)[k_j]
+    {
+        double h[6];
+#pragma unroll
+        for (int ra = 0; ra < 6; ++ra) {
+            // E_i = [e_k, -S(d_l) row k]: -S(d) rows (0, d2, -d1), (-d2, 0, d0), (d1, -d0, 0)
+            const double e3 = (k == 0) ? 0.0 : (k == 1) ? -dl[2] : dl[1];
+            const double e4 = (k == 0) ? dl[2] : (k == 1) ? 0.0 : -dl[0];
+            const double e5 = (k == 0) ? -dl[1] : (k == 1) ? dl[0] : 0.0;
+            const double hk = (k == 0) ? R.S[ra][0] : (k == 1) ? R.S[ra][1] : R.S[ra][2];
+            h[ra] = hk + e3 * R.S[ra][3] + e4 * R.S[ra][4] + e5 * R.S[ra][5];
+        }
+#pragma unroll
+        for (int lj = 0; lj < 4; ++lj) {
+            const double dj[3] = {P.d[3 * lj], P.d[3 * lj + 1], P.d[3 * lj + 2]};
+            double cr[3];
+            cross3(dj, &h[3], cr);
+#pragma unroll
+            for (int kj = 0; kj < 3; ++kj) hrow[3 * lj + kj] = ((3 * lj + kj == i) ? 1.0 : 0.0) + h[kj] - cr[kj];
+        }
+        // g_f = g_s - E_i Mb^-1 v,  g_s = -E_i (W + [0, 0, g / m, 0, 0, 0])
+        double wv[6];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) wv[c] = P.W[c] + (c == 2 ? pr.gravity * inv_m : 0.0) + uv[c];
+        double cw[3];
+        cross3(dl, &wv[3], cw);
+        gsv = -(((k == 0) ? wv[0] : (k == 1) ? wv[1] : wv[2]) - ((k == 0) ? cw[0] : (k == 1) ? cw[1] : cw[2]));
+    }
+    UST(ka, rb, 13);  // Y, H_f row, g_f
+    // Nt row j = (Mbj Y)_j Mb^-1 E^T + Jbj column j; t0_j = bbj_j + Mbj row j . q0
+    const int j = i;
+    {
+        double my[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, t4[2] = {0.0, 0.0}, s2 = 0.0;
+#pragma unroll
+        for (int kk = 0; kk < 12; ++kk) {
+            const double mk = P.Mbj[j * 12 + kk], jc = P.Jbj[kk * 12 + j];
+#pragma unroll
+            for (int c = 0; c < 6; ++c) my[c] = fma(mk, R.Y[kk][c], my[c]);
+            t4[kk & 1] = fma(mk, R.q0[kk], t4[kk & 1]);
+            s2 = fma(mk, mk, fma(jc, jc, s2));
+        }
+        double mm[6];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) mm[c] = my[c] * inv_m;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) mm[3 + c] = P.Icinv[3 * c] * my[3] + P.Icinv[3 * c + 1] * my[4] + P.Icinv[3 * c + 2] * my[5];
+        double nt[12];
+#pragma unroll
+        for (int lj = 0; lj < 4; ++lj) {
+            const double dj[3] = {P.d[3 * lj], P.d[3 * lj + 1], P.d[3 * lj + 2]};
+            double cr[3];
+            cross3(dj, &mm[3], cr);
+#pragma unroll
+            for (int kj = 0; kj < 3; ++kj) nt[3 * lj + kj] = mm[kj] - cr[kj] + P.Jbj[(3 * lj + kj) * 12 + j];
+        }
         if (ok && wr && lane < 12) {
-            *reinterpret_cast<double2*>(&pre->Nt[j * 12 + c]) = make_double2(v0, v1);
-            *reinterpret_cast<double2*>(&pre->P[j * 12 + c]) = make_double2(X[j][c], X[j][c + 1]);
+#pragma unroll
+            for (int c = 0; c < 12; c += 2)
+                *reinterpret_cast<double2*>(&pre->Nt[j * 12 + c]) = make_double2(nt[c], nt[c + 1]);
+#pragma unroll
+            for (int c = 0; c < 6; c += 2) *reinterpret_cast<double2*>(&pre->Y[j * 6 + c]) = make_double2(yi[c], yi[c + 1]);
+            pre->q0[j] = R.q0[j];
+            pre->t0[j] = P.bbj[j] + (t4[0] + t4[1]);
+            pre->nsel[j] = s2;
         }
     }
-    if (ok && wr && lane < 12) {
-        pre->q0[j] = X[j][12];
-        pre->t0[j] = t0;
-        pre->nsel[j] = s2;
-    }
-    lds_sync();  // X (aliasing L) is read completely before the factorisation writes L
+    lds_sync();  // the scratch (aliasing the factor's L) is read completely before factor12 writes L
+    UST(ka, rb, 14);  // Nt, t0, record stores
     return ok;
 }
 
@@ -714,7 +867,7 @@ __device__ bool stance_reduce(const Prob& P, const wbc_params& pr, int lane, boo
 // own scratch); lane = lane within the robot's segment; wr = false for a padding segment past the
 // batch (computes a duplicate robot, writes nothing to HBM).
 template <int SUB>
-__device__ void update_phase(const KernelArgs& a, int rb, int lane, bool wr, UpdScratch& s, Prob& P, Presolve* pre,
+__device__ bool update_phase(const KernelArgs& a, int rb, int lane, bool wr, UpdScratch& s, Prob& P, Presolve* pre,
                              const wbc_model& md) {
     const wbc_params& pr = *a.params;
     const int kap = a.contacts[rb];
@@ -1328,8 +1481,8 @@ __device__ void update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
         double hrow[12], gsv = 0.0;
         bool stance = false;
         if constexpr (SUB == 16) {
-            if (WBC_STANCE_ELIM && (kap == 15 || a.modes))
-                stance = stance_reduce(P, pr, lane, wr, s.ps.L, s.ps.ild, hrow, gsv, pre);
+            if (WBC_STANCE_ELIM && a.elim && (kap == 15 || a.modes))
+                stance = stance_reduce(a, rb, P, pr, lane, wr, s, hrow, gsv, pre);
         }
         const bool fact = stance || !a.modes;
         if (fact) {
@@ -1344,15 +1497,18 @@ __device__ void update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
                 if (lane < 12) pre->xs[lane] = s.ps.xs[lane];
             }
             if (lane == 0 && !ok && !a.modes) P.flags += 2.0;
-            if (lane == 0 && !ok && stance) stance = false;  // modes: the kappa = 15 hypothesis factors H_s itself
+            stance = stance && ok;  // (ok is uniform over the segment) modes: the kappa = 15 hypothesis factors H_s itself
         }
         if (lane == 0 && wr) {
             pre->presolved = (fact && !stance) ? 1.0 : 0.0;
             pre->stance = stance ? 1.0 : 0.0;
         }
         lds_sync();
+        UST(a, rb, 11);  // slot 19; slots 20.. belong to the solve (EST)
+        return stance;
     }
     UST(a, rb, 11);  // slot 19; slots 20.. belong to the solve (EST)
+    return false;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2228,8 +2384,9 @@ static_assert(offsetof(Presolve, t0) == 104 * sizeof(double) && offsetof(Presolv
 // (same QP restricted to the equality manifold), which the iteration-parity tests check.
 //   friction face rr of leg l:  -D_rr f_l >= 0                       (cpp:404-424)
 //   torque row j, sign sg:      sg (t0_j - Nt_j f) >= -tau_max       (cpp:495,506,513)
-__device__ void solve_stance(const KernelArgs& a, int rb, const Prob& P, const PreRegs& pf, const Presolve* rec,
+__device__ void solve_stance(const KernelArgs& a, int rb, const Prob* Pg, const PreRegs& pf, const Presolve* rec,
                              StanceScratch& s) {
+    const Prob& P = *Pg;  // the assembled problem in HBM / L2: only flags, bbar_j and the x-output fields are read
     constexpr int N = StanceScratch::N, MC = StanceScratch::MC, NEQ = 12;
     const wbc_params& pr = *a.params;
     const int lane = lane_id();
@@ -2492,55 +2649,55 @@ __device__ void solve_stance(const KernelArgs& a, int rb, const Prob& P, const P
     }
     lds_sync();
     const bool ok = (status == WBC_QP_OK);
-    // torques tau_j = t0_j - Nt_j f (cpp:565-576), grf = f (cpp:556-563), qdd = q0 - P f
+    // torques tau_j = t0_j - Nt_j f (cpp:565-576), grf = f (cpp:556-563)
     const double t0j = vbcast(pf.v1, 40 + (lane < 12 ? lane : 0));  // all lanes: ds_bpermute reads 0 from inactive ones
     if (lane < 12) {
         const int j = lane;
         const double2* nt = reinterpret_cast<const double2*>(rec->Nt + j * 12);
-        const double2* pp = reinterpret_cast<const double2*>(rec->P + j * 12);
-        double t4[4] = {0.0, 0.0, 0.0, 0.0}, q4[4] = {0.0, 0.0, 0.0, 0.0};
+        double t4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int c = 0; c < 12; c += 2) {
             const double2 nv = nt[c / 2];
             t4[c & 3] = fma(nv.x, s.ucon[c], t4[c & 3]);
             t4[(c + 1) & 3] = fma(nv.y, s.ucon[c + 1], t4[(c + 1) & 3]);
-            if (a.x) {
-                const double2 pv = pp[c / 2];
-                q4[c & 3] = fma(pv.x, s.ucon[c], q4[c & 3]);
-                q4[(c + 1) & 3] = fma(pv.y, s.ucon[c + 1], q4[(c + 1) & 3]);
-            }
         }
         const double tv = t0j - ((t4[0] + t4[1]) + (t4[2] + t4[3]));
         a.tau[(size_t)rb * 12 + lane] = ok ? tv : 0.0;
         a.grf[(size_t)rb * 12 + lane] = ok ? s.ucon[j] : 0.0;
-        if (a.x) s.ucon[12 + j] = rec->q0[j] - ((q4[0] + q4[1]) + (q4[2] + q4[3]));
     }
-    if (a.x) {
-        lds_sync();
+    if (a.x) {  // x (42, cpp:534-541): a = Mb^-1 (E^T f - gw), qdd = q0 - Y Mb^-1 E^T f, f, slacks |rsw|
+        double F[3] = {0, 0, 0}, Mm[3] = {0, 0, 0};
+#pragma unroll
+        for (int ll = 0; ll < 4; ++ll) {
+            const double fl[3] = {s.ucon[3 * ll], s.ucon[3 * ll + 1], s.ucon[3 * ll + 2]};
+            const double dl[3] = {P.d[3 * ll], P.d[3 * ll + 1], P.d[3 * ll + 2]};
+            double t[3];
+            cross3(dl, fl, t);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) { F[i] += fl[i]; Mm[i] += t[i]; }
+        }
+        double bf[6];  // Mb^-1 E^T f
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            bf[i] = F[i] * P.inv_m;
+            bf[3 + i] = P.Icinv[3 * i] * Mm[0] + P.Icinv[3 * i + 1] * Mm[1] + P.Icinv[3 * i + 2] * Mm[2];
+        }
         if (lane < 42) {
             double xv;
-            if (lane < 6) {  // a = Mbar_b^-1 (Jc_com^T f - gw)
-                double F[3] = {0, 0, 0}, Mm[3] = {0, 0, 0};
-#pragma unroll
-                for (int ll = 0; ll < 4; ++ll) {
-                    const double fl[3] = {s.ucon[3 * ll], s.ucon[3 * ll + 1], s.ucon[3 * ll + 2]};
-                    const double dl[3] = {P.d[3 * ll], P.d[3 * ll + 1], P.d[3 * ll + 2]};
-                    double t[3];
-                    cross3(dl, fl, t);
-#pragma unroll
-                    for (int i = 0; i < 3; ++i) { F[i] += fl[i]; Mm[i] += t[i]; }
-                }
-                if (lane < 3) xv = sel3(F, lane) * P.inv_m - (lane == 2 ? pr.gravity : 0.0);
-                else {
-                    const int r3 = lane - 3;
-                    xv = P.Icinv[3 * r3] * Mm[0] + P.Icinv[3 * r3 + 1] * Mm[1] + P.Icinv[3 * r3 + 2] * Mm[2];
-                }
+            if (lane < 6) {
+                xv = sel3(bf, lane < 3 ? lane : 0);
+                xv = (lane < 3) ? xv - (lane == 2 ? pr.gravity : 0.0) : sel3(&bf[3], lane < 3 ? 0 : lane - 3);
             } else if (lane < 18) {
-                xv = s.ucon[12 + lane - 6];
+                const int j = lane - 6;
+                const double* yr = rec->Y + j * 6;
+                double qv = rec->q0[j];
+#pragma unroll
+                for (int c = 0; c < 6; ++c) qv = fma(-yr[c], bf[c], qv);
+                xv = qv;
             } else if (lane < 30) {
                 xv = s.ucon[lane - 18];
             } else {
-                xv = fabs(P.rsw[lane - 30]);
+                xv = a.modes ? 0.0 : fabs(P.rsw[lane - 30]);  // hypotheses mask the swing bound of stance legs
             }
             a.x[(size_t)rb * WBC_NV + lane] = ok ? xv : 0.0;
         }
@@ -2593,7 +2750,7 @@ struct SolveLds {
     Prob prob;
     union {
         QpScratch q;
-        StanceScratch st;
+        StanceScratch st;  // the combined form (WBC_STANCE_KERNEL 0): stance QPs in this kernel
     };
 };
 
@@ -2628,18 +2785,69 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_kernel(KernelArgs a) {
     lds_sync();
     // work row: [Prob | Presolve]; the Presolve record is stored by update_phase itself
     Presolve* pre = reinterpret_cast<Presolve*>(a.work + (size_t)rb * WORK_LEN + PROB_LEN);
-    update_phase<UPD_SUB>(a, rb, lane, wr, L.u[seg], L.prob[seg], pre, L.model);
+    if (a.elim && blockIdx.x == 0 && threadIdx.x == 0) a.fb[a.parity ^ 1] = 0;  // for the next update
+    const bool stance = update_phase<UPD_SUB>(a, rb, lane, wr, L.u[seg], L.prob[seg], pre, L.model);
     const double2* src = reinterpret_cast<const double2*>(&L.prob[seg]);
     double2* dst = reinterpret_cast<double2*>(a.work + (size_t)rb * WORK_LEN);
     if (wr) {
         for (int k = lane; k < PROB_LEN / 2; k += UPD_SUB) dst[k] = src[k];
     }
+    // mask-15 QPs whose elimination failed go to the fallback list (rare: one atomic each)
+    if (WBC_STANCE_ELIM && a.elim && wr && !stance) {
+        const int K = a.modes;
+        const bool mine = K ? (lane < K && (a.mode_masks[lane < K ? lane : 0] & 15) == 15)
+                            : (lane == 0 && (a.contacts[rb] & 15) == 15);
+        if (mine) {
+            const int idx = atomicAdd(&a.fb[a.parity], 1);
+            a.fb[2 + idx] = K ? rb * K + lane : rb;
+        }
+    }
 }
+
+// Four-contact QP whose equalities the update kernel eliminated (its Presolve::stance flag, in
+// the record registers): wbc_solve_stance_kernel's; every other QP is wbc_solve_kernel's.
+__device__ __forceinline__ int qp_mask(const KernelArgs& a, int rb, int row) {
+    return a.modes ? (a.mode_masks[rb - row * a.modes] & 15) : (a.contacts[rb] & 15);
+}
+
+__device__ void solve_general_qp(const KernelArgs& a, int rb, SolveLds& L);
 
 WBC_KERNEL_ATTR void wbc_solve_kernel(KernelArgs a) {
     __shared__ SolveLds L;
     const int rb = xcd_robot();
     if (rb >= a.batch) return;
+    if (!WBC_STANCE_KERNEL && WBC_STANCE_ELIM && a.elim) {
+        // combined form: a step with the elimination on is all mask 15 (bar mode hypotheses), so
+        // waiting for the record flag before the problem copy costs the rare general QP only
+        const int row = a.modes ? rb / a.modes : rb;
+        const double* prow = a.work + (size_t)row * WORK_LEN + PROB_LEN;
+        PreRegs pf;
+        pf.v0 = prow[lane_id()];
+        pf.v1 = prow[64 + lane_id()];
+        if (bcast(pf.v1, PRE_STANCE - 64) != 0.0 && (!a.modes || qp_mask(a, rb, row) == 15)) {
+            solve_stance(a, rb, reinterpret_cast<const Prob*>(a.work + (size_t)row * WORK_LEN), pf,
+                         reinterpret_cast<const Presolve*>(prow), L.st);
+            return;
+        }
+    }
+    solve_general_qp(a, rb, L);
+}
+
+// The general solve of the elimination fallbacks (mask-15 QPs with a near-singular leg), after
+// the stance kernel: a few workgroups stride over the list, whose length the host does not know
+// (usually 0).  The loop keeps the kernel arguments live through the solve (spills): this is the
+// rare path; wbc_solve_kernel is the straight-line one.
+WBC_KERNEL_ATTR void wbc_solve_fallback_kernel(KernelArgs a) {
+    __shared__ SolveLds L;
+    const int n = a.fb[a.parity];
+    for (int w = blockIdx.x; w < n; w += gridDim.x) {
+        const int rb = a.fb[2 + w];
+        wsync();
+        solve_general_qp(a, rb, L);
+    }
+}
+
+__device__ void solve_general_qp(const KernelArgs& a, int rb, SolveLds& L) {
     // mode hypotheses: QP rb is hypothesis rb % modes of state rb / modes (one assembled problem
     // per state, read by all of its hypotheses)
     const int row = a.modes ? rb / a.modes : rb;
@@ -2647,10 +2855,14 @@ WBC_KERNEL_ATTR void wbc_solve_kernel(KernelArgs a) {
     const double* prow = a.work + (size_t)row * WORK_LEN + PROB_LEN;
     PreRegs pf;
     pf.v0 = prow[lane_id()];
-    pf.v1 = prow[lane_id() < PRE_LEN - 64 ? 64 + lane_id() : PRE_LEN - 1];
+    pf.v1 = prow[64 + lane_id()];
+    const int kap_qp = qp_mask(a, rb, row);
     double2* dst = reinterpret_cast<double2*>(&L.prob);
     const double2* src = reinterpret_cast<const double2*>(a.work + (size_t)row * WORK_LEN);
     for (int k = lane_id(); k < PROB_LEN / 2; k += 64) dst[k] = src[k];
+    // the stance kernel's QP: checked after the problem copy is issued, so that a general QP's
+    // loads all go out together (one HBM round trip)
+    if (WBC_STANCE_KERNEL && WBC_STANCE_ELIM && a.elim && kap_qp == 15 && bcast(pf.v1, PRE_STANCE - 64) != 0.0) return;
     if (a.modes) {  // this hypothesis' contact mask on the unmasked bounds (update_phase)
         const int kap = a.mode_masks[rb - row * a.modes] & 15;
         const int lane = lane_id();
@@ -2662,10 +2874,31 @@ WBC_KERNEL_ATTR void wbc_solve_kernel(KernelArgs a) {
         if (lane == 0) L.prob.kappa = (double)kap;
     }
     wsync();
-    if (WBC_STANCE_ELIM && (int)L.prob.kappa == 15 && bcast(pf.v1, PRE_STANCE - 64) != 0.0)
-        solve_stance(a, rb, L.prob, pf, reinterpret_cast<const Presolve*>(prow), L.st);
-    else
-        solve_phase(a, rb, L.prob, &pf, L.q);
+    solve_phase(a, rb, L.prob, &pf, L.q);
+}
+
+// Four-contact stance QPs whose equalities the update kernel eliminated (Presolve::stance) are
+// solved here, in the 12-variable force space; wbc_solve_kernel skips them.  A kernel of its own
+// so that its register and LDS budgets (no 24-variable state, no LDS copy of the problem) allow
+// WBC_STANCE_WAVES waves per SIMD instead of the general solve's 2.
+#ifndef WBC_STANCE_WAVES
+#define WBC_STANCE_WAVES 3  // 2 and 3 time the same; 4 spills (profiles/r02/d)
+#endif
+__global__ __attribute__((amdgpu_flat_work_group_size(64, 64), amdgpu_waves_per_eu(WBC_STANCE_WAVES)))
+void wbc_solve_stance_kernel(KernelArgs a) {
+    __shared__ StanceScratch S;
+    const int rb = blockIdx.x;
+    if (rb >= a.batch) return;
+    const int row = a.modes ? rb / a.modes : rb;
+    const double* prow = a.work + (size_t)row * WORK_LEN + PROB_LEN;
+    PreRegs pf;
+    pf.v0 = prow[lane_id()];
+    pf.v1 = prow[64 + lane_id()];
+    // the engine turns the elimination on only when every QP has mask 15; an elimination
+    // fallback (near-singular leg, Presolve::stance = 0) is wbc_solve_fallback_kernel's
+    if (bcast(pf.v1, PRE_STANCE - 64) == 0.0 || (a.modes && qp_mask(a, rb, row) != 15)) return;
+    solve_stance(a, rb, reinterpret_cast<const Prob*>(a.work + (size_t)row * WORK_LEN), pf,
+                 reinterpret_cast<const Presolve*>(prow), S);
 }
 
 __global__ void wbc_reset_kernel(double* hist, const uint8_t* mask, int batch) {
@@ -2684,12 +2917,22 @@ extern "C" hipError_t wbc_launch_step(const wbc::KernelArgs* a, hipStream_t st) 
     return hipGetLastError();
 }
 extern "C" int wbc_kernel_default_split() { return WBC_DEFAULT_SPLIT; }
+extern "C" int wbc_kernel_stance_elim() { return WBC_STANCE_ELIM; }
 extern "C" hipError_t wbc_launch_update(const wbc::KernelArgs* a, hipStream_t st) {
     hipLaunchKernelGGL(wbc::wbc_update_kernel, dim3((a->batch + wbc::UPD_RPW - 1) / wbc::UPD_RPW), dim3(64), 0, st, *a);
     return hipGetLastError();
 }
-extern "C" hipError_t wbc_launch_solve(const wbc::KernelArgs* a, hipStream_t st) {
+// The split step's solve: the general kernel (one workgroup per QP), or, when the engine turned
+// the stance elimination on, the stance kernel (one workgroup per QP) and the fallback kernel.
+extern "C" hipError_t wbc_launch_solve_general(const wbc::KernelArgs* a, hipStream_t st) {
     hipLaunchKernelGGL(wbc::wbc_solve_kernel, dim3(a->batch), dim3(64), 0, st, *a);
+    return hipGetLastError();
+}
+extern "C" hipError_t wbc_launch_solve_stance(const wbc::KernelArgs* a, hipStream_t st) {
+    if (!WBC_STANCE_ELIM) return hipSuccess;
+    if (!WBC_STANCE_KERNEL) return wbc_launch_solve_general(a, st);
+    hipLaunchKernelGGL(wbc::wbc_solve_stance_kernel, dim3(a->batch), dim3(64), 0, st, *a);
+    hipLaunchKernelGGL(wbc::wbc_solve_fallback_kernel, dim3(16), dim3(64), 0, st, *a);
     return hipGetLastError();
 }
 extern "C" hipError_t wbc_launch_reset(double* hist, const uint8_t* mask, int batch, hipStream_t st) {

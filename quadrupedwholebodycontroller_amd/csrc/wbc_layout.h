@@ -50,11 +50,11 @@ constexpr int PROB_LEN = sizeof(Prob) / sizeof(double);
 // after the problem in the work row and read by the solve kernel from HBM / L2.
 //
 // Four-contact stance (kappa = 15) is solved in a smaller space: the 12 stance equalities
-// (R1, cpp:494,504) Jbar_c,j qdd + G f = e are solved for qdd = q0 - P f (Gauss-Jordan with
-// partial pivoting in the update kernel), which leaves a 12-variable QP in the contact forces
-// with Hessian H_f = P^T P + H_s and gradient g_s - P^T q0, and only inequality rows
-// (16 friction faces, 24 torque rows tau = t0 - Nt f).  Then Mi / xs hold the factor of H_f and
-// the unconstrained f0, and the stance fields below are filled.
+// (R1, cpp:494,504) Jbar_c,j qdd + G f = e are solved for qdd = q0 - P f in the update kernel,
+// which leaves a 12-variable QP in the contact forces with Hessian H_f = P^T P + H_s and gradient
+// g_s - P^T q0, and only inequality rows (16 friction faces, 24 torque rows tau = t0 - Nt f).
+// Then Mi / xs hold the factor of H_f and the unconstrained f0, and the stance fields below are
+// filled (wbc_kernel.hip stance_reduce).
 struct Presolve {
     double Mi[78];    // M = L^-1 of the slot Hessian H_s = L L^T (H_f for stance), lower triangle row-major
     double xs[12];    // slot part of the unconstrained optimum x0 = -H^-1 g (f0 for stance)
@@ -64,7 +64,7 @@ struct Presolve {
     double t0[12];    //         tau = t0 - Nt f  (t0 = bbar_j + Mbar_j q0)
     double nsel[12];  //         |row|^2 of torque row j in the reference's 42-variable space
     double Nt[144];   //         Nt = Mbar_j P + Jbar_c,j^T, [joint j][force c]
-    double P[144];    //         P = Jbar_c,j^-1 G, [joint][force]
+    double Y[72];     //         P = Y B^T (rank 6): qdd = q0 - Y [F / m; I_c^-1 sum d_l x f_l], [joint][6]
 };
 static_assert(sizeof(Presolve) % 16 == 0, "Presolve must keep 16-byte alignment");
 constexpr int PRE_LEN = sizeof(Presolve) / sizeof(double);
@@ -94,7 +94,16 @@ struct KernelArgs {
     int32_t cold;       // stateful, but no QP hotstart (WBC_COLD)
     int32_t modes;      // contact-mode hypotheses per state (wbc_step_modes); 0 = one QP per input row
     const uint8_t* mode_masks;  // [modes]: contact mask of hypothesis k
+    // Four-contact stance elimination (Presolve::stance) for this step's mask-15 QPs: the engine
+    // turns it on when every QP of the step has mask 15 (then the stance solve kernel runs
+    // instead of the general one).  Mask-15 QPs whose elimination fails (a near-singular leg)
+    // are listed for the fallback solve: fb[parity] counts them, fb[2 ..] lists them; the update
+    // kernel clears fb[parity ^ 1] for the next update.
+    int32_t elim;
+    int32_t parity;
+    int32_t* fb;
 };
+
 
 
 }  // namespace wbc

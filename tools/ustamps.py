@@ -23,5 +23,13 @@ du = np.diff(u, axis=1)
 ok = (u > 0).all(1)
 res = {n: float(np.median(du[ok, i])) for i, n in enumerate(un)}
 res["total (stamps 0..11)"] = float(np.median(u[ok, -1] - u[ok, 0]))
+# four-contact stance stage inside the presolve slot (stamps 12..14, written before stamp 11)
+st = e.debug()[0::4, 20:23]
+ok2 = ok & (st > 0).all(1)
+if ok2.any():
+    res["stance: Gauss-Jordan"] = float(np.median(st[ok2, 0] - u[ok2, 10]))
+    res["stance: H_f row"] = float(np.median(st[ok2, 1] - st[ok2, 0]))
+    res["stance: Nt, t0, stores"] = float(np.median(st[ok2, 2] - st[ok2, 1]))
+    res["stance: factor H_f + stores"] = float(np.median(u[ok2, 11] - st[ok2, 2]))
 res["robots sampled"] = int(ok.sum())
 print(json.dumps(dict(config=cfg, batch=B, split_update_cycles=res), indent=1))
