@@ -50,48 +50,79 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(inp, budget_s=15.0, threads=None):
-    """Time the CPU restatement of the reference path (oracle/wbc_ref.c through ctypes, which releases
-    the GIL) on a bounded sample of the same inputs: `threads` host threads, each solving a contiguous
-    slice (robots are independent, as in the reference's one-controller-per-robot deployment), plus a
-    shorter single-thread run.  threads defaults to min(16, os.cpu_count()) (the GPU box's CPU share)."""
-    import ctypes  # noqa: F401
-    from concurrent.futures import ThreadPoolExecutor
+def _native_baseline_lib():
+    """Build the CPU baseline with -march=native for this host into a temp dir; the
+    portable x86-64-v3 build (oracle/_build/libwbc_ref.so) if that fails.  Returns (path or None, note)."""
+    import tempfile
 
+    out = os.path.join(tempfile.gettempdir(), f"wbc_cpu_native_{os.getpid()}.so")
+    try:
+        r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "native", f"NATIVE_OUT={out}"],
+                           capture_output=True, text=True, timeout=120)
+        if r.returncode == 0 and os.path.exists(out):
+            return out, "-O3 -march=native -fopenmp (built on this host)"
+        return None, "-O3 -march=x86-64-v3 -fopenmp (native build failed: %s)" % r.stderr.strip()[-200:]
+    except (OSError, subprocess.SubprocessError) as ex:
+        return None, "-O3 -march=x86-64-v3 -fopenmp (native build failed: %s)" % ex
+
+
+def cpu_baseline(inp, budget_s=15.0, threads=None):
+    """Time the CPU restatements on a bounded sample of the same inputs (inputs cycled), one robot
+    per OpenMP thread (static schedule), as SURVEY.md 8d prescribes, in two variants:
+      * structure-exploiting (oracle/wbc_fast.c): the GPU engine's algorithm (closed-form
+        centroidal transform, reduced QP, stance elimination) -> the reported `value`;
+      * reference-faithful (oracle/wbc_ref.c): dense 18x18 LU inverses, dense 42 x 70 active set.
+    Each on `threads` threads (default min(16, nproc): the GPU box's CPU share, OMP_NUM_THREADS
+    there) and on one thread."""
     lib_path = os.path.join(ROOT, "oracle", "_build", "libwbc_ref.so")
     B = inp["base_pose"].shape[0]
     if not os.path.exists(lib_path):
         return _cpu_baseline_numpy(inp, budget_s)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import wbc_ref  # ctypes wrapper of the C restatement
+    import wbc_ref  # ctypes wrapper of the C restatements
 
-    T = threads or max(1, min(16, os.cpu_count() or 1))
+    T = threads or max(1, min(16, os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+    native, build_note = _native_baseline_lib()
 
     def sample(n):
         idx = np.arange(n) % B
         return {k: np.ascontiguousarray(v[idx]) for k, v in inp.items()}
 
-    def run(n, nthreads, budget):
+    def run(variant, n, nthreads, budget):
         t_used = 0.0
         while True:
             sub = sample(n)
-            bounds = [(i * n // nthreads, (i + 1) * n // nthreads) for i in range(nthreads)]
-            parts = [{k: v[a:b] for k, v in sub.items()} for a, b in bounds]
-            with ThreadPoolExecutor(nthreads) as ex:
-                t0 = time.perf_counter()
-                list(ex.map(wbc_ref.run_batch, parts))
-                dt = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            wbc_ref.cpu_run_batch(sub, variant, nthreads, native)
+            dt = time.perf_counter() - t0
             t_used += dt
             if dt >= 0.8 * budget or t_used >= 2.5 * budget:
                 return n, dt
             n = int(n * max(2.0, min(10.0, budget / max(dt, 1e-6))))
 
-    n1, dt1 = run(64, 1, budget_s / 3)
-    nT, dtT = run(64 * T, T, budget_s)
-    return dict(value=nT / dtT, unit="solves/s", cores=T, kind="port",
-                sample=f"{nT} cold solves of the same workload (inputs cycled) through oracle/wbc_ref.c (dense "
-                       f"reference-faithful restatement, -O3), {T} host threads, {dtT:.2f} s",
-                single_core=dict(value=n1 / dt1, cores=1, sample=f"{n1} cold solves, 1 thread, {dt1:.2f} s"))
+    res = {}
+    for variant, share in (("fast", 0.5), ("dense", 0.5)):
+        b = budget_s * share
+        n1, dt1 = run(variant, 64, 1, b / 4)
+        nT, dtT = run(variant, 64 * T, T, 3 * b / 4)
+        res[variant] = dict(value=nT / dtT, unit="solves/s", cores=T, kind="port",
+                            sample=f"{nT} cold solves of the same workload (inputs cycled), {T} OpenMP threads, "
+                                   f"{dtT:.2f} s",
+                            single_core=dict(value=n1 / dt1, cores=1, sample=f"{n1} cold solves, 1 thread, {dt1:.2f} s"))
+    if native:
+        try:
+            os.remove(native)
+        except OSError:
+            pass
+    out = dict(res["fast"])
+    out["variant"] = ("structure-exploiting (oracle/wbc_fast.c: the engine's algorithm - closed-form centroidal "
+                      "transform, reduced QP, four-contact equality elimination - dense Goldfarb-Idnani per robot)")
+    out["build"] = build_note
+    out["reference_faithful"] = dict(res["dense"], variant="oracle/wbc_ref.c: seven dense 18x18 LU inverses, dense "
+                                                         "42 x 70 Goldfarb-Idnani (src/whole_body_controller.cpp:256-542)")
+    out["note"] = (f"{T} threads is the GPU box's CPU share (OMP_NUM_THREADS); the box's other cores belong to "
+                   f"other jobs, so the all-core figure is not taken")
+    return out
 
 
 def _cpu_baseline_numpy(inp, budget_s):
@@ -369,9 +400,12 @@ def main():
         torch.cuda.synchronize()
         return ev0.elapsed_time(ev1) / args.steps
 
-    # A step is two kernels (wbc_step's default form): the update kernel (dynamics + assembly, four
-    # robots per wave) then the solve kernel (QP + torques).  Each is timed alone on the launch
-    # stream; the dominant one (the solve kernel) carries the roofline.
+    # A step is the update kernel (dynamics + assembly, four robots per wave) then the solve: for an
+    # all-stance batch (the engine's choice) the stance solve kernel and the fallback
+    # kernel, otherwise the general solve kernel.  Each part is timed alone on the launch stream;
+    # the dominant one carries the roofline.
+    elim = (not K) and bool(np.all((inp["contacts"] & 15) == 15))
+    solve_name = "wbc_solve_stance_kernel" if elim else "wbc_solve_kernel"
     step_ms = timed(lambda: step(STEP_FLAGS))
     out = e.outputs()
     iters = out["iters"].astype(np.int64)
@@ -388,13 +422,13 @@ def main():
     else:
         upd_ms = timed(lambda: e.update(STEP_FLAGS))
         solve_ms = timed(lambda: e.solve(STEP_FLAGS))  # re-solves the assembled problem (stateless)
-    kernels = {"wbc_update_kernel": upd_ms, "wbc_solve_kernel": solve_ms}
+    kernels = {"wbc_update_kernel": upd_ms, solve_name: solve_ms}
     dom = max(kernels, key=kernels.get)
     dom_ms = kernels[dom]
     # flops owned by each kernel: dynamics + assembly in the update, factorisation + active-set
-    # iterations + torques in the solve
+    # iterations + torques in the solve (SURVEY 8d's dense-problem counts, whatever form computes them)
     flops_k = {"wbc_update_kernel": float(S * (F_DYN + F_ASM)),
-               "wbc_solve_kernel": float(np.sum(F_TAU + F_FACT + F_ITER * iters))}
+               solve_name: float(np.sum(F_TAU + F_FACT + F_ITER * iters))}
     tf_dom = flops_k[dom] / (dom_ms * 1e-3) / 1e12
     bytes_step = S * BYTES_IN + B * BYTES_OUT
     hbm_gbs = bytes_step / (step_ms * 1e-3) / 1e9
@@ -415,12 +449,20 @@ def main():
                 step2(STEP_FLAGS)
             ms2 = timed(lambda: step2(STEP_FLAGS))
             o2 = e2.outputs()
+            tr2, tr2_src = committed_traffic(name, B2)
             extra[name] = dict(batch=B2, ms_per_step=ms2, solves_per_s=B2 / (ms2 * 1e-3),
                                status_counts=np.bincount(o2["status"], minlength=4).tolist(),
-                               mean_iters=float(o2["iters"].mean()), desc=c2["desc"])
+                               mean_iters=float(o2["iters"].mean()), desc=c2["desc"],
+                               traffic_per_step=tr2.get("step"), traffic_source=tr2_src,
+                               algorithmic_bytes_per_step=float((B2 // (c2.get("modes") or 1)) * BYTES_IN +
+                                                                B2 * BYTES_OUT))
             e2.close()
 
     traffic, traffic_src = committed_traffic(args.config, B)
+    if elim and traffic:  # the stance solve is two launches (the fallback kernel is near empty)
+        traffic = dict(traffic)
+        traffic["wbc_solve_stance_kernel"] = (traffic.get("wbc_solve_stance_kernel") or 0.0) + \
+            (traffic.get("wbc_solve_fallback_kernel") or 0.0)
     total = (B * world if scaling == "weak" else B_total) * args.steps
     value = total / elapsed
     result = {
@@ -450,7 +492,7 @@ def main():
                              "k = iters[] per robot); latency/issue-bound small dense linear algebra"},
         "roofline_hbm": {"bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": hbm_gbs / HBM_PEAK_GBS, "bytes_per_solve": bytes_step / B,
-                         "traffic": (traffic.get("wbc_update_kernel", 0) + traffic.get("wbc_solve_kernel", 0))
+                         "traffic": (traffic.get("wbc_update_kernel", 0) + traffic.get(solve_name, 0))
                          if traffic else None,
                          "note": "algorithmic bytes over the step (both kernels): 729 B read per state + 200 B "
                                  "written per QP (929 B/solve one QP per state); traffic = PMC bytes per step "

@@ -589,6 +589,12 @@ static int solve_qp(const double* H, const double* g, const double* A, const dou
     return gi_solve(n, H, g, me, CE, ce, mi, CI, ci, max_iter, warm, nwarm, x, iters, act_out, nact_out);
 }
 
+/* The dense Goldfarb-Idnani above for other callers (oracle/wbc_fast.c), cold (no warm set). */
+int wbc_ref_gi(int n, const double* H, const double* g, int me, const double* CE, const double* ce, int mi, const double* CI,
+               const double* ci, int max_iter, double* x, int* iters) {
+    return gi_solve(n, H, g, me, CE, ce, mi, CI, ci, max_iter, NULL, 0, x, iters, NULL, NULL);
+}
+
 /* ------------------------------------------------------------------ controller */
 void wbc_ref_state_init(wbc_ref_state* s) { /* setInitialState, cpp:65-120 (history part) */
     memset(s, 0, sizeof(*s));
@@ -693,7 +699,7 @@ int wbc_ref_step(const wbc_model* md, const wbc_params* pr, wbc_ref_state* st, c
         for (int i = 0; i < ND * ND; ++i) st->Tdot_inv[i] = -st->Tdot_inv[i];
     }
     /* solveQP (cpp:466-542) */
-    static double H[NV * NV], A[NC * NV];
+    static _Thread_local double H[NV * NV], A[NC * NV];  /* per thread: the CPU baseline runs robots in parallel */
     double g[NV], lb[NC], ub[NC], W[6];
     {
         const int sl = 6 + NJ + 3 * NL;

@@ -36,6 +36,18 @@ int wbc_ref_step(const wbc_model* md, const wbc_params* pr, wbc_ref_state* st, c
 void wbc_ref_run_batch(const wbc_model* md, const wbc_params* pr, int B, const double* pose, const double* nu,
                        const double* qj, const double* ref, const uint8_t* contacts, const uint8_t* switching, double* tau,
                        double* grf, double* x, int32_t* status, int32_t* iters);
+int wbc_ref_gi(int n, const double* H, const double* g, int me, const double* CE, const double* ce, int mi, const double* CI,
+               const double* ci, int max_iter, double* x, int* iters);
+
+/* CPU baseline (bench.py cpu_baseline): oracle/wbc_fast.c, structure-exploiting, cold steps */
+int wbc_fast_step(const wbc_model* md, const wbc_params* pr, const double* pose, const double* nu, const double* qj,
+                  const double* ref, int contacts, double* tau, double* grf, int* iters);
+void wbc_fast_run_batch(const wbc_model* md, const wbc_params* pr, int B, const double* pose, const double* nu,
+                        const double* qj, const double* ref, const uint8_t* contacts, double* tau, double* grf,
+                        int32_t* status, int32_t* iters, int threads);
+void wbc_ref_run_batch_omp(const wbc_model* md, const wbc_params* pr, int B, const double* pose, const double* nu,
+                           const double* qj, const double* ref, const uint8_t* contacts, const uint8_t* switching,
+                           double* tau, double* grf, int32_t* status, int32_t* iters, int threads);
 
 #ifdef __cplusplus
 }

@@ -51,7 +51,48 @@ def lib():
         _lib.wbc_ref_step.argtypes = [P, P, P, P, P, P, P, C.c_int, C.c_int, P, P, P, P, P]
         _lib.wbc_ref_step.restype = C.c_int
         _lib.wbc_ref_run_batch.argtypes = [P, P, C.c_int, P, P, P, P, P, P, P, P, P, P, P]
+        _bind_baseline(_lib)
     return _lib
+
+
+def _bind_baseline(L):
+    P = C.c_void_p
+    L.wbc_fast_run_batch.argtypes = [P, P, C.c_int, P, P, P, P, P, P, P, P, P, C.c_int]
+    L.wbc_ref_run_batch_omp.argtypes = [P, P, C.c_int, P, P, P, P, P, P, P, P, P, P, C.c_int]
+
+
+_baseline_libs = {}
+
+
+def baseline_lib(path=None):
+    """The CPU-baseline library: `path` (e.g. a -march=native build, oracle/Makefile `native`) or
+    the portable build."""
+    if path is None:
+        return lib()
+    if path not in _baseline_libs:
+        L = C.CDLL(path)
+        _bind_baseline(L)
+        _baseline_libs[path] = L
+    return _baseline_libs[path]
+
+
+def cpu_run_batch(inp, variant="fast", threads=1, libpath=None):
+    """Cold batch on `threads` OpenMP threads through the CPU baseline: variant "fast"
+    (oracle/wbc_fast.c, structure-exploiting) or "dense" (oracle/wbc_ref.c, reference-faithful)."""
+    m, p = model_params()
+    B = inp["base_pose"].shape[0]
+    f = lambda k, dt=np.float64: np.ascontiguousarray(inp[k], dt)
+    pose, nu, qj, ref = f("base_pose"), f("nu"), f("qj"), f("ref")
+    con, sw = f("contacts", np.uint8), f("switching", np.uint8)
+    out = dict(tau=np.zeros((B, 12)), grf=np.zeros((B, 12)), status=np.zeros(B, np.int32), iters=np.zeros(B, np.int32))
+    L = baseline_lib(libpath)
+    if variant == "fast":
+        L.wbc_fast_run_batch(C.byref(m), C.byref(p), B, _p(pose), _p(nu), _p(qj), _p(ref), _p(con), _p(out["tau"]),
+                             _p(out["grf"]), _p(out["status"]), _p(out["iters"]), int(threads))
+    else:
+        L.wbc_ref_run_batch_omp(C.byref(m), C.byref(p), B, _p(pose), _p(nu), _p(qj), _p(ref), _p(con), _p(sw),
+                                _p(out["tau"]), _p(out["grf"]), _p(out["status"]), _p(out["iters"]), int(threads))
+    return out
 
 
 def _model_params():

@@ -2390,6 +2390,7 @@ __device__ void solve_stance(const KernelArgs& a, int rb, const Prob* Pg, const 
     constexpr int N = StanceScratch::N, MC = StanceScratch::MC, NEQ = 12;
     const wbc_params& pr = *a.params;
     const int lane = lane_id();
+    STAMP(a, rb, 0);
     int status = (P.flags != 0.0) ? WBC_QP_NUMERIC : WBC_QP_OK;
     int iters = 0;
     // M (packed p < 78: M(i, j), p = i (i + 1) / 2 + j) and f0 (78..89) from the record registers
@@ -2453,6 +2454,7 @@ __device__ void solve_stance(const KernelArgs& a, int rb, const Prob* Pg, const 
         nn = (np[0] + np[1]) + (np[2] + np[3]);
         sp = ((sq[0] + sq[1]) + (sq[2] + sq[3])) - bp;
     }
+    STAMP(a, rb, 1);  // unpack, normals, norms, slacks
     {   // C0[:, p] = M n_p (M read as a broadcast)
         double t[N];
 #pragma unroll
@@ -2473,6 +2475,7 @@ __device__ void solve_stance(const KernelArgs& a, int rb, const Prob* Pg, const 
     zero_rinv(s);
     lds_sync();
 
+    STAMP(a, rb, 2);  // C0, zero R^-1
     int q = 0;         // active set size
     double u = 0.0;    // multiplier of active slot `lane`
     int act = -1;      // constraint (lane) of active slot `lane`
@@ -2622,6 +2625,7 @@ __device__ void solve_stance(const KernelArgs& a, int rb, const Prob* Pg, const 
         }
     }
 
+    STAMP(a, rb, 3);  // active-set loop
     // primal: f = f0 + H_f^-1 N_A u = f0 + M^T w',  w' = sum_s u_s C0[:, a_s]
     double wi;
     {
@@ -2648,6 +2652,7 @@ __device__ void solve_stance(const KernelArgs& a, int rb, const Prob* Pg, const 
         if (lane < N) s.ucon[lane] = s.xs[i] + ((x4[0] + x4[1]) + (x4[2] + x4[3]));
     }
     lds_sync();
+    STAMP(a, rb, 4);  // primal
     const bool ok = (status == WBC_QP_OK);
     // torques tau_j = t0_j - Nt_j f (cpp:565-576), grf = f (cpp:556-563)
     const double t0j = vbcast(pf.v1, 40 + (lane < 12 ? lane : 0));  // all lanes: ds_bpermute reads 0 from inactive ones
@@ -2706,6 +2711,7 @@ __device__ void solve_stance(const KernelArgs& a, int rb, const Prob* Pg, const 
         a.status[rb] = status;
         a.iters[rb] = iters;
     }
+    STAMP(a, rb, 5);  // outputs
     if (Hh) {  // working set for the next cycle's hotstart, in the general numbering
         const unsigned long long am = __ballot(is_con && active) << NEQ;
         if (lane == 0) {
@@ -2881,6 +2887,9 @@ __device__ void solve_general_qp(const KernelArgs& a, int rb, SolveLds& L) {
 // solved here, in the 12-variable force space; wbc_solve_kernel skips them.  A kernel of its own
 // so that its register and LDS budgets (no 24-variable state, no LDS copy of the problem) allow
 // WBC_STANCE_WAVES waves per SIMD instead of the general solve's 2.
+#ifndef WBC_AB_NO_FALLBACK
+#define WBC_AB_NO_FALLBACK 0
+#endif
 #ifndef WBC_STANCE_WAVES
 #define WBC_STANCE_WAVES 3  // 2 and 3 time the same; 4 spills (profiles/r02/d)
 #endif
@@ -2932,7 +2941,8 @@ extern "C" hipError_t wbc_launch_solve_stance(const wbc::KernelArgs* a, hipStrea
     if (!WBC_STANCE_ELIM) return hipSuccess;
     if (!WBC_STANCE_KERNEL) return wbc_launch_solve_general(a, st);
     hipLaunchKernelGGL(wbc::wbc_solve_stance_kernel, dim3(a->batch), dim3(64), 0, st, *a);
-    hipLaunchKernelGGL(wbc::wbc_solve_fallback_kernel, dim3(16), dim3(64), 0, st, *a);
+    if (!WBC_AB_NO_FALLBACK)  // A/B measurement builds only (-DWBC_AB_NO_FALLBACK=1): not a correct solve
+        hipLaunchKernelGGL(wbc::wbc_solve_fallback_kernel, dim3(16), dim3(64), 0, st, *a);
     return hipGetLastError();
 }
 extern "C" hipError_t wbc_launch_reset(double* hist, const uint8_t* mask, int batch, hipStream_t st) {

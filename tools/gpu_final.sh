@@ -1,19 +1,24 @@
-# Round-end evidence on one GPU box: GPU tests, smoke, the default bench line (with the CPU
-# baseline), the --extra configs, a rocprofv3 kernel-trace summary of the same bench command, and
-# the PMC passes (separate runs) whose summary bench.py reads for roofline.traffic.
+# Round evidence on one GPU box: GPU tests, smoke, PMC passes for the bench workloads (separate
+# runs; their summaries under profiles/$ROUND/ are what bench.py reads for roofline.traffic), the
+# default bench line (with the CPU baseline), the --extra configs, and a rocprofv3 kernel-trace
+# summary of the same bench command.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 TAG=${TAG:-final}
+ROUND=${ROUND:-r02}
 O=gpurun_out/$TAG
-mkdir -p $O
+mkdir -p $O profiles/$ROUND
 step() { local name=$1 t=$2; shift 2; echo "== $name $(date +%T)"; timeout -k 10 $t "$@" > $O/$name.log 2>&1; local rc=$?; echo "== $name rc=$rc"; if [ $rc -ne 0 ]; then tail -30 $O/$name.log; exit $rc; fi; }
 step pytest 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
 step smoke 120 python -c "import __graft_entry__ as g; g.smoke()"
-step pmc 600 env TAG=$TAG bash tools/pmc.sh
-cp gpurun_out/pmc_$TAG/pmc_summary.json $O/pmc_stance_cold_b4096.json
-cp $O/pmc_stance_cold_b4096.json profiles/r01/pmc_stance_cold_b4096.json  # read by bench.py below
+for cb in stance_cold_b4096:4096 rl_random_b8192:8192 modes16_b16384:16384; do
+  c=${cb%%:*}; b=${cb##*:}
+  step pmc_$c 600 env TAG=${TAG}_$c CONFIG=$c BATCH=$b bash tools/pmc.sh
+  cp gpurun_out/pmc_${TAG}_$c/pmc_summary.json $O/pmc_$c.json
+  cp $O/pmc_$c.json profiles/$ROUND/pmc_$c.json  # read by bench.py below
+done
 step bench 300 python bench.py --steps 50 --warmup 5
-step bench_extra 300 python bench.py --steps 20 --warmup 3 --extra --breakdown --no-cpu-baseline
+step bench_extra 300 python bench.py --steps 20 --warmup 3 --extra --no-cpu-baseline
 step prof 300 rocprofv3 --kernel-trace --stats -d $O/prof -o prof --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline
 tail -1 $O/bench.log
 echo final done
