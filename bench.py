@@ -427,8 +427,12 @@ def main():
     dom_ms = kernels[dom]
     # flops owned by each kernel: dynamics + assembly in the update, factorisation + active-set
     # iterations + torques in the solve (SURVEY 8d's dense-problem counts, whatever form computes them)
-    flops_k = {"wbc_update_kernel": float(S * (F_DYN + F_ASM)),
-               solve_name: float(np.sum(F_TAU + F_FACT + F_ITER * iters))}
+    # An all-stance step factors the QP in the update kernel (the equality elimination and the
+    # force-space Cholesky), so F_fact is the update kernel's there; otherwise the
+    # solve kernel's equality block is the counterpart of the reference's initial factorisation.
+    f_fact_upd = F_FACT if elim else 0
+    flops_k = {"wbc_update_kernel": float(S * (F_DYN + F_ASM + f_fact_upd)),
+               solve_name: float(np.sum(F_TAU + (F_FACT - f_fact_upd) + F_ITER * iters))}
     tf_dom = flops_k[dom] / (dom_ms * 1e-3) / 1e12
     bytes_step = S * BYTES_IN + B * BYTES_OUT
     hbm_gbs = bytes_step / (step_ms * 1e-3) / 1e9
@@ -488,8 +492,11 @@ def main():
                      "traffic_source": traffic_src, "kernel": dom, "kernel_ms": dom_ms,
                      "kernels_ms": kernels, "step_kernels_ms": step_ms,
                      "note": "dominant kernel; fp64 VALU roof (no MFMA on this path; gfx950 fp64 vector peak); "
-                             "algorithmic flops of SURVEY 8(d) owned by this kernel (F_fact + F_tau + k F_iter, "
-                             "k = iters[] per robot); latency/issue-bound small dense linear algebra"},
+                             "algorithmic flops of SURVEY 8(d) owned by this kernel: update = F_dyn + F_asm (+ F_fact "
+                             "on an all-stance step, whose factorisation runs there), solve = F_tau + k F_iter (+ "
+                             "F_fact otherwise), k = iters[] per robot; latency/issue-bound small dense linear "
+                             "algebra",
+                     "flops_per_launch": flops_k[dom]},
         "roofline_hbm": {"bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": hbm_gbs / HBM_PEAK_GBS, "bytes_per_solve": bytes_step / B,
                          "traffic": (traffic.get("wbc_update_kernel", 0) + traffic.get(solve_name, 0))
