@@ -17,6 +17,7 @@ extern "C" hipError_t wbc_launch_step(const wbc::KernelArgs* a, hipStream_t st);
 extern "C" hipError_t wbc_launch_update(const wbc::KernelArgs* a, hipStream_t st);
 extern "C" hipError_t wbc_launch_solve_general(const wbc::KernelArgs* a, hipStream_t st);
 extern "C" hipError_t wbc_launch_solve_stance(const wbc::KernelArgs* a, hipStream_t st);
+extern "C" hipError_t wbc_launch_update_solve(const wbc::KernelArgs* a, hipStream_t st);
 extern "C" int wbc_kernel_default_split();
 extern "C" hipError_t wbc_launch_reset(double* hist, const uint8_t* mask, int batch, hipStream_t st);
 extern "C" int wbc_kernel_stance_elim();
@@ -161,6 +162,12 @@ void begin_update(wbc_engine* h, wbc::KernelArgs& a) {
     a.elim = h->elim ? 1 : 0;
     a.parity = h->elim_parity;
 }
+
+// Stateless all-stance wbc_step: update and stance solve in one kernel (wbc_update_solve_kernel);
+// 0 keeps the separate stance solve kernel (A/B builds)
+#ifndef WBC_INLINE_STANCE
+#define WBC_INLINE_STANCE 1
+#endif
 
 hipError_t launch_solves(wbc_engine* h, wbc::KernelArgs& a) {
     a.elim = h->elim ? 1 : 0;
@@ -421,8 +428,13 @@ int32_t wbc_step(wbc_engine* h, uint32_t flags) {
     const bool split = (flags & WBC_SPLIT) || (!(flags & WBC_FUSED) && wbc_kernel_default_split());
     if (split) {
         begin_update(h, a);
-        WBC_HIP(wbc_launch_update(&a, h->stream));
-        WBC_HIP(launch_solves(h, a));
+        if (h->elim && !a.stateful && WBC_INLINE_STANCE) {
+            // stateless all-stance step: the update kernel solves the stance QPs itself
+            WBC_HIP(wbc_launch_update_solve(&a, h->stream));
+        } else {
+            WBC_HIP(wbc_launch_update(&a, h->stream));
+            WBC_HIP(launch_solves(h, a));
+        }
     } else {
         WBC_HIP(wbc_launch_step(&a, h->stream));
     }

@@ -81,6 +81,26 @@ struct UpdScratch {
     double yv[6];           // Tdot_inv nu exchange (segmented update kernel)
 };
 
+// The update kernel's inline stance solve (solve_stance16) works in the robot's own UpdScratch,
+// in arrays the update no longer reads once stance_reduce has formed Nt: the force-space factor
+// M and f0 stay where factor12 leaves them (ps.L, ps.xs), the rest goes here.
+struct St16 {
+    double* Nt;    // [12][12] torque map rows (ja .. A: 204 doubles)
+    double* Y;     // [12][6]  (in)
+    double* t0;    // [12]     (in + 72)
+    double* q0;    // [12]     (sc)
+    double* nsel;  // [12]     (sc + 12): |reference torque row|^2
+    double* col;   // [16]     column exchange: d (12), slack, Givens pair (KA)
+    double* ucon;  // [48]     multiplier per constraint (Mjj, hj)
+    double* f;     // [12]     primal forces (cen)
+    __device__ explicit St16(UpdScratch& s)
+        : Nt(&s.ja[0][0]), Y(&s.in[0]), t0(&s.in[72]), q0(&s.sc[0][0]), nsel(&s.sc[6][0]), col(&s.KA[0][0]),
+          ucon(&s.Mjj[0][0]), f(&s.cen[0]) {}
+};
+static_assert(offsetof(UpdScratch, A) + sizeof(UpdScratch::A) - offsetof(UpdScratch, ja) >= 144 * sizeof(double), "St16 Nt");
+static_assert(offsetof(UpdScratch, hj) == offsetof(UpdScratch, Mjj) + sizeof(UpdScratch::Mjj), "St16 ucon");
+static_assert(sizeof(UpdScratch::hj) + sizeof(UpdScratch::Mjj) >= 48 * sizeof(double), "St16 ucon");
+
 struct QpScratch {
     static constexpr int N = NQ;
     double L[12][13];       // Cholesky factor of the slot Hessian (row-major, lower); then M = L^-1
@@ -619,6 +639,9 @@ __device__ __forceinline__ int seg16_argmax(double v) {
 // rows' reference-space norms), H_f row i and g_f in hrow / gsv for factor12.  Returns false
 // (nothing usable stored; the caller takes the general path) at a near-singular leg or S.
 // Lane i < 12 of the segment is row i = 3 l + k; SUB = 16 only (one robot per DPP row).
+// SOLVE (the update kernel's inline stance solve, wbc_update_solve_kernel): Nt, Y, q0, t0 and the
+// norms stay in the robot's LDS scratch (St16) instead of going to the Presolve record.
+template <bool SOLVE>
 __device__ bool stance_reduce([[maybe_unused]] const KernelArgs& ka, [[maybe_unused]] int rb, const Prob& P,
                               const wbc_params& pr, int lane, bool wr, UpdScratch& s, double (&hrow)[12],
                               double& gsv, Presolve* pre) {
@@ -843,7 +866,19 @@ __device__ bool stance_reduce([[maybe_unused]] const KernelArgs& ka, [[maybe_unu
 #pragma unroll
             for (int kj = 0; kj < 3; ++kj) nt[3 * lj + kj] = mm[kj] - cr[kj] + P.Jbj[(3 * lj + kj) * 12 + j];
         }
-        if (ok && wr && lane < 12) {
+        if constexpr (SOLVE) {
+            const St16 V(s);
+            if (lane < 12) {
+#pragma unroll
+                for (int c = 0; c < 12; c += 2)
+                    *reinterpret_cast<double2*>(&V.Nt[j * 12 + c]) = make_double2(nt[c], nt[c + 1]);
+#pragma unroll
+                for (int c = 0; c < 6; c += 2) *reinterpret_cast<double2*>(&V.Y[j * 6 + c]) = make_double2(yi[c], yi[c + 1]);
+                V.q0[j] = R.q0[j];
+                V.t0[j] = P.bbj[j] + (t4[0] + t4[1]);
+                V.nsel[j] = s2;
+            }
+        } else if (ok && wr && lane < 12) {
 #pragma unroll
             for (int c = 0; c < 12; c += 2)
                 *reinterpret_cast<double2*>(&pre->Nt[j * 12 + c]) = make_double2(nt[c], nt[c + 1]);
@@ -860,13 +895,339 @@ __device__ bool stance_reduce([[maybe_unused]] const KernelArgs& ka, [[maybe_unu
 }
 
 // ---------------------------------------------------------------------------------------
+// inline stance solve: the 12-variable force-space QP of a four-contact robot whose equalities
+// stance_reduce eliminated, solved by its own 16-lane segment of the update wave (four robots per
+// wave) right after factor12, so that nothing of it passes through HBM.  The same Goldfarb-Idnani
+// steps as solve_stance (same selection, ratio tests, Householder add and Givens drop, the same
+// arithmetic order in every column and slack), with the 40 inequality rows dealt three to a lane:
+// lane l holds friction face l (slot 0), torque row 16 + l (slot 1) and, for l < 8, torque row
+// 32 + l (slot 2).  R^-1 lives in registers (lane i < 12: row i).  Cold start only (the engine
+// uses it for stateless all-stance steps); primal recovery f = f0 + M^T M (N_A u).
+// ---------------------------------------------------------------------------------------
+// min over each 16-lane DPP row of a value tagged with a 6-bit index (as wave_argmin_lane: ties to
+// the lowest index); returns the index, uniform over the row
+__device__ __forceinline__ double tag6(double v, int idx) {
+    const int hi = __double2hiint(v);
+    const int tag = (hi < 0) ? (63 - idx) : idx;
+    return __hiloint2double(hi, (__double2loint(v) & ~63) | tag);
+}
+__device__ __forceinline__ double seg16_min(double v) {
+    v = fmin(v, dpp_d<0x128>(v));
+    v = fmin(v, dpp_d<0x124>(v));
+    v = fmin(v, dpp_d<0x122>(v));
+    v = fmin(v, dpp_d<0x121>(v));
+    return v;
+}
+__device__ __forceinline__ int untag6(double v) {
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    return (hi < 0) ? (63 - (lo & 63)) : (lo & 63);
+}
+// lane j of the caller's 16-lane segment (dynamic j; ds_bpermute, every lane of the segment active)
+__device__ __forceinline__ double seg_shfl(double v, int j) { return vbcast(v, ((int)threadIdx.x & ~15) + (j & 15)); }
+__device__ __forceinline__ int seg_shfl_i(int v, int j) {
+    return __builtin_amdgcn_ds_bpermute((((int)threadIdx.x & ~15) + (j & 15)) << 2, v);
+}
+__device__ __forceinline__ double sel3d(int j, double a, double b, double c) { return j == 0 ? a : (j == 1 ? b : c); }
+
+__device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, const Prob& P, UpdScratch& s) {
+    constexpr int N = 12;
+    const wbc_params& pr = *a.params;
+    const St16 V(s);
+    const double (&Mi)[12][12] = *reinterpret_cast<const double(*)[12][12]>(&s.ps.L[0][0]);
+    const double* f0 = s.ps.xs;
+    int status = (P.flags != 0.0) ? WBC_QP_NUMERIC : WBC_QP_OK;
+    int iters = 0;
+    lds_sync();
+
+    // normals (force space) of the three slots, as solve_stance / build_normal
+    const int fl = l >> 2, rr = l & 3, k1 = l >> 1, k2 = 8 + ((l & 7) >> 1);
+    const bool v2 = l < 8;
+    const double sg = (l & 1) ? -1.0 : 1.0;
+    double c0[N], c1[N], c2[N];
+#pragma unroll
+    for (int m = 0; m < N; ++m) {
+        const int r = m % 3;
+        const double fv = (r == 0) ? ((rr == 0) ? -1.0 : (rr == 1 ? 1.0 : 0.0))
+                        : (r == 1) ? ((rr == 2) ? -1.0 : (rr == 3 ? 1.0 : 0.0)) : pr.friction;
+        c0[m] = (m / 3 == fl) ? fv : 0.0;
+        c1[m] = -sg * V.Nt[k1 * 12 + m];
+        c2[m] = v2 ? -sg * V.Nt[k2 * 12 + m] : 0.0;
+    }
+    const double bp1 = -pr.max_torque - sg * V.t0[k1], bp2 = -pr.max_torque - sg * V.t0[k2];
+    const double tol0 = 1e-10;
+    const double tol1 = 1e-10 * fmax(1.0, fabs(-pr.max_torque - sg * P.bbj[k1]));
+    const double tol2 = 1e-10 * fmax(1.0, fabs(-pr.max_torque - sg * P.bbj[k2]));
+    const double in0 = 1.0 / sqrt(fmax(1.0 + pr.friction * pr.friction, 1e-300));
+    const double in1 = 1.0 / sqrt(fmax(V.nsel[k1], 1e-300)), in2 = 1.0 / sqrt(fmax(V.nsel[k2], 1e-300));
+    double sp0, sp1, sp2;
+    {
+        double q0[4] = {0.0, 0.0, 0.0, 0.0}, q1[4] = {0.0, 0.0, 0.0, 0.0}, q2[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            const double x = f0[j];
+            q0[j & 3] += c0[j] * x;
+            q1[j & 3] += c1[j] * x;
+            q2[j & 3] += c2[j] * x;
+        }
+        sp0 = ((q0[0] + q0[1]) + (q0[2] + q0[3])) - 0.0;
+        sp1 = ((q1[0] + q1[1]) + (q1[2] + q1[3])) - bp1;
+        sp2 = ((q2[0] + q2[1]) + (q2[2] + q2[3])) - bp2;
+    }
+    {   // C0 = M n
+        double t0[N], t1[N], t2[N];
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            double a0[4] = {0.0, 0.0, 0.0, 0.0}, a1[4] = {0.0, 0.0, 0.0, 0.0}, a2[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int j = 0; j <= i; ++j) {
+                const double m = Mi[i][j];
+                a0[j & 3] += m * c0[j];
+                a1[j & 3] += m * c1[j];
+                a2[j & 3] += m * c2[j];
+            }
+            t0[i] = (a0[0] + a0[1]) + (a0[2] + a0[3]);
+            t1[i] = (a1[0] + a1[1]) + (a1[2] + a1[3]);
+            t2[i] = (a2[0] + a2[1]) + (a2[2] + a2[3]);
+        }
+#pragma unroll
+        for (int i = 0; i < N; ++i) { c0[i] = t0[i]; c1[i] = t1[i]; c2[i] = t2[i]; }
+    }
+    double rinv[N];  // row l of R^-1 (l < 12)
+#pragma unroll
+    for (int k = 0; k < N; ++k) rinv[k] = 0.0;
+    int q = 0, pstar = -1, act = -1, ab = 0;  // ab: bit j = slot j of this lane active
+    double u = 0.0, up = 0.0;
+    bool done = (status != WBC_QP_OK);
+    const int max_wsr = pr.max_wsr;
+
+    while (__any(!done)) {
+        if (!done) {
+            if (pstar < 0) {  // most violated row, by slack / |reference row|
+                const double w0 = (!(ab & 1) && sp0 < -tol0) ? sp0 * in0 : 1e300;
+                const double w1 = (!(ab & 2) && sp1 < -tol1) ? sp1 * in1 : 1e300;
+                const double w2 = (v2 && !(ab & 4) && sp2 < -tol2) ? sp2 * in2 : 1e300;
+                const double m = seg16_min(fmin(tag6(w0, l), fmin(tag6(w1, 16 + l), tag6(w2, 32 + l))));
+                if (!(m < 1e299)) done = true;  // optimal
+                pstar = untag6(m);
+                up = 0.0;
+            }
+            if (!done && ++iters > max_wsr) { status = WBC_QP_MAX_ITER; iters = max_wsr; done = true; }
+        }
+        if (!done) {
+            const int pos = q, ol = pstar & 15, js = pstar >> 4;
+            if (l == ol) {
+#pragma unroll
+                for (int k = 0; k < N; ++k) V.col[k] = sel3d(js, c0[k], c1[k], c2[k]);
+                V.col[12] = sel3d(js, sp0, sp1, sp2);
+            }
+            lds_sync();
+            double d[N], d2[N];
+#pragma unroll
+            for (int k = 0; k < N; ++k) d[k] = V.col[k];
+            const double sps = V.col[12];
+            lds_sync();
+            double rk;
+            {
+                double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int k = 0; k < N; ++k) acc[k & 3] += rinv[k] * d[k];
+                rk = l < N ? (acc[0] + acc[1]) + (acc[2] + acc[3]) : 0.0;
+            }
+            double cz0, cz1, cz2, cq0, cq1, cq2, zn, dq;
+            {
+                double z0[4] = {0, 0, 0, 0}, z1[4] = {0, 0, 0, 0}, z2[4] = {0, 0, 0, 0}, zz[4] = {0, 0, 0, 0};
+                double e0[4] = {0, 0, 0, 0}, e1[4] = {0, 0, 0, 0}, e2[4] = {0, 0, 0, 0}, ee[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int j = 0; j < N; ++j) {
+                    const double mk = (j >= pos) ? 1.0 : 0.0, ok = (j == pos) ? 1.0 : 0.0;
+                    d2[j] = d[j] * mk;
+                    z0[j & 3] += c0[j] * d2[j]; z1[j & 3] += c1[j] * d2[j]; z2[j & 3] += c2[j] * d2[j];
+                    zz[j & 3] += d[j] * d2[j];
+                    e0[j & 3] += c0[j] * ok; e1[j & 3] += c1[j] * ok; e2[j & 3] += c2[j] * ok;
+                    ee[j & 3] += d[j] * ok;
+                }
+                cz0 = (z0[0] + z0[1]) + (z0[2] + z0[3]); cz1 = (z1[0] + z1[1]) + (z1[2] + z1[3]);
+                cz2 = (z2[0] + z2[1]) + (z2[2] + z2[3]); zn = (zz[0] + zz[1]) + (zz[2] + zz[3]);
+                cq0 = (e0[0] + e0[1]) + (e0[2] + e0[3]); cq1 = (e1[0] + e1[1]) + (e1[2] + e1[3]);
+                cq2 = (e2[0] + e2[1]) + (e2[2] + e2[3]); dq = (ee[0] + ee[1]) + (ee[2] + ee[3]);
+            }
+            // step: t1 (drop an active slot) or t2 (the new row becomes active)
+            const double vt = (l < q && rk > 1e-14) ? u * fast_rcp(rk) : 1e300;
+            const int l1 = untag6(seg16_min(tag6(vt, l)));
+            const double t1 = seg_shfl(vt, l1);
+            const double t2 = (zn > 1e-14) ? (-sps * fast_rcp(zn)) : 1e300;
+            const double t = fmin(t1, t2);
+            if (!(t < 1e299)) {
+                status = WBC_QP_INFEASIBLE;
+                done = true;
+            } else {
+                const bool full = (t2 < 1e299 && t2 <= t1);
+                if (t2 < 1e299) { sp0 += t * cz0; sp1 += t * cz1; sp2 += t * cz2; }
+                if (l < q) u -= t * rk;
+                up += t;
+                const bool add = full;
+                if (!full) {
+                    const int dropped = seg_shfl_i(act, l1);
+                    if (l == (dropped & 15)) ab &= ~(1 << (dropped >> 4));
+                    const double un = seg_shfl(u, l + 1);
+                    const int an = seg_shfl_i(act, l + 1);
+                    if (l >= l1 && l < q - 1) { u = un; act = an; }
+                    if (l == q - 1) { u = 0.0; act = -1; }
+                    --q;
+                }
+                {   // Householder add (householder_masked), on the three slots; no-op on a drop
+                    const double zn_ = add ? zn : 1.0, dq_ = add ? dq : 0.0;
+                    const double rs = fast_rsq(zn_);
+                    const double nrm2 = zn_ * rs;
+                    const double alpha = (dq_ >= 0.0) ? -nrm2 : nrm2;
+                    const double ia = (dq_ >= 0.0) ? -rs : rs;
+                    const double beta = fast_rcp(zn_ + nrm2 * fabs(dq_));
+                    const double vw0 = add ? (cz0 - alpha * cq0) * beta : 0.0;
+                    const double vw1 = add ? (cz1 - alpha * cq1) * beta : 0.0;
+                    const double vw2 = add ? (cz2 - alpha * cq2) * beta : 0.0;
+                    const double va0 = vw0 * alpha, va1 = vw1 * alpha, va2 = vw2 * alpha;
+#pragma unroll
+                    for (int k = 0; k < N; ++k) {
+                        const double ok = (k == pos) ? 1.0 : 0.0;
+                        c0[k] = fma(va0, ok, fma(-vw0, d2[k], c0[k]));
+                        c1[k] = fma(va1, ok, fma(-vw1, d2[k], c1[k]));
+                        c2[k] = fma(va2, ok, fma(-vw2, d2[k], c2[k]));
+                    }
+                    const double nv = (l == pos) ? ia : -rk * ia;
+                    const bool wcol = add && l <= pos;
+#pragma unroll
+                    for (int k = 0; k < N; ++k) rinv[k] = (wcol && k == pos) ? nv : rinv[k];
+                }
+                if (add) {
+                    if (l == q) { u = up; act = pstar; }
+                    if (l == ol) ab |= 1 << js;
+                    ++q;
+                    pstar = -1;
+                } else {
+                    // Givens deletion of slot l1 (givens_drop): rotations on rows (k, k+1), k = l1..q-1,
+                    // from the column of the constraint now in slot k (its owner lane, via LDS)
+#pragma unroll
+                    for (int k = 0; k < N - 1; ++k) {
+                        if (k >= l1 && k < q) {
+                            const int pl = seg_shfl_i(act, k);
+                            if (l == (pl & 15)) {
+                                const int jx = pl >> 4;
+                                V.col[13] = sel3d(jx, c0[k], c1[k], c2[k]);
+                                V.col[14] = sel3d(jx, c0[k + 1], c1[k + 1], c2[k + 1]);
+                            }
+                            lds_sync();
+                            const double a0 = V.col[13], b0 = V.col[14];
+                            lds_sync();
+                            const double r2 = a0 * a0 + b0 * b0;
+                            const double rh = (r2 > 0.0) ? fast_rsq(r2) : 0.0;
+                            const double c = (r2 > 0.0) ? a0 * rh : 1.0, sn = b0 * rh;
+                            double x, y;
+                            x = c0[k]; y = c0[k + 1]; c0[k] = fma(c, x, sn * y); c0[k + 1] = fma(c, y, -sn * x);
+                            x = c1[k]; y = c1[k + 1]; c1[k] = fma(c, x, sn * y); c1[k + 1] = fma(c, y, -sn * x);
+                            x = c2[k]; y = c2[k + 1]; c2[k] = fma(c, x, sn * y); c2[k + 1] = fma(c, y, -sn * x);
+                            x = rinv[k]; y = rinv[k + 1]; rinv[k] = fma(c, x, sn * y); rinv[k + 1] = fma(c, y, -sn * x);
+                        }
+                    }
+                    const int src = l + ((l >= l1) ? 1 : 0);
+#pragma unroll
+                    for (int k = 0; k < N; ++k) {
+                        const double v = seg_shfl(rinv[k], src);
+                        rinv[k] = (l < q && k >= l && k < q) ? v : 0.0;
+                    }
+                }
+            }
+        }
+    }
+
+    // primal: f = f0 + M^T M (N_A u), N_A u = sum over active rows of u_p n_p (original normals)
+    V.ucon[l] = 0.0;
+    V.ucon[16 + l] = 0.0;
+    V.ucon[32 + l] = 0.0;
+    lds_sync();
+    if (l < q) V.ucon[act] = u;
+    lds_sync();
+    double nu[N];
+    {
+        const double u0 = V.ucon[l], u1 = V.ucon[16 + l], u2 = v2 ? V.ucon[32 + l] : 0.0;
+#pragma unroll
+        for (int m = 0; m < N; ++m) {
+            const int r = m % 3;
+            const double fv = (r == 0) ? ((rr == 0) ? -1.0 : (rr == 1 ? 1.0 : 0.0))
+                            : (r == 1) ? ((rr == 2) ? -1.0 : (rr == 3 ? 1.0 : 0.0)) : pr.friction;
+            const double n0 = (m / 3 == fl) ? fv : 0.0;
+            const double n1 = -sg * V.Nt[k1 * 12 + m], n2 = v2 ? -sg * V.Nt[k2 * 12 + m] : 0.0;
+            nu[m] = seg_sum<16>(fma(u2, n2, fma(u1, n1, u0 * n0)));
+        }
+    }
+    const int i = l < N ? l : 0;
+    double zi;
+    {
+        double z4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k = 0; k < N; ++k) z4[k & 3] += Mi[i][k] * nu[k];
+        zi = (z4[0] + z4[1]) + (z4[2] + z4[3]);
+    }
+    {
+        double x4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k = 0; k < N; ++k) x4[k & 3] += Mi[k][i] * seg_bcast<16>(zi, k);
+        if (l < N) V.f[l] = f0[i] + ((x4[0] + x4[1]) + (x4[2] + x4[3]));
+    }
+    lds_sync();
+    const bool ok = (status == WBC_QP_OK);
+    if (wr && l < N) {  // tau_j = t0_j - Nt_j f (cpp:565-576), grf = f (cpp:556-563)
+        double t4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int c = 0; c < 12; ++c) t4[c & 3] = fma(V.Nt[l * 12 + c], V.f[c], t4[c & 3]);
+        const double tv = V.t0[l] - ((t4[0] + t4[1]) + (t4[2] + t4[3]));
+        a.tau[(size_t)rb * 12 + l] = ok ? tv : 0.0;
+        a.grf[(size_t)rb * 12 + l] = ok ? V.f[l] : 0.0;
+    }
+    if (a.x && wr) {  // x (42, cpp:534-541): a = Mb^-1 (E^T f - gw), qdd = q0 - Y Mb^-1 E^T f, f, |rsw|
+        double F[3] = {0, 0, 0}, Mm[3] = {0, 0, 0};
+#pragma unroll
+        for (int ll = 0; ll < 4; ++ll) {
+            const double fv[3] = {V.f[3 * ll], V.f[3 * ll + 1], V.f[3 * ll + 2]};
+            const double dl[3] = {P.d[3 * ll], P.d[3 * ll + 1], P.d[3 * ll + 2]};
+            double t[3];
+            cross3(dl, fv, t);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) { F[c] += fv[c]; Mm[c] += t[c]; }
+        }
+        double bf[6];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            bf[c] = F[c] * P.inv_m;
+            bf[3 + c] = P.Icinv[3 * c] * Mm[0] + P.Icinv[3 * c + 1] * Mm[1] + P.Icinv[3 * c + 2] * Mm[2];
+        }
+        if (l < 12) {
+            double* xr = a.x + (size_t)rb * WBC_NV;
+            if (l < 6) xr[l] = ok ? ((l < 3) ? sel3(bf, l < 3 ? l : 0) - (l == 2 ? pr.gravity : 0.0)
+                                             : sel3(&bf[3], l < 3 ? 0 : l - 3)) : 0.0;
+            double qv = V.q0[l];
+#pragma unroll
+            for (int c = 0; c < 6; ++c) qv = fma(-V.Y[l * 6 + c], bf[c], qv);
+            xr[6 + l] = ok ? qv : 0.0;
+            xr[18 + l] = ok ? V.f[l] : 0.0;
+            xr[30 + l] = ok ? fabs(P.rsw[l]) : 0.0;
+        }
+    }
+    if (wr && l == 0) {
+        a.status[rb] = status;
+        a.iters[rb] = iters;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 // update phase (≙ updateState, cpp:256-294, plus the per-cycle terms of solveQP that do not
 // depend on the QP: computeDesiredWrench cpp:426-445, swing commands cpp:447-464, bounds cpp:503-515)
 // ---------------------------------------------------------------------------------------
 // SUB = lanes per robot (64: one robot per wave; 16 / 32: 4 / 2 robots per wave, each with its
 // own scratch); lane = lane within the robot's segment; wr = false for a padding segment past the
 // batch (computes a duplicate robot, writes nothing to HBM).
-template <int SUB>
+// SOLVE: a four-contact robot whose elimination succeeded is solved here too (solve_stance16) and
+// its Presolve record is not written (wbc_update_solve_kernel; the return value says which).
+template <int SUB, bool SOLVE = false>
 __device__ bool update_phase(const KernelArgs& a, int rb, int lane, bool wr, UpdScratch& s, Prob& P, Presolve* pre,
                              const wbc_model& md) {
     const wbc_params& pr = *a.params;
@@ -1482,13 +1843,20 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
         bool stance = false;
         if constexpr (SUB == 16) {
             if (WBC_STANCE_ELIM && a.elim && (kap == 15 || a.modes))
-                stance = stance_reduce(a, rb, P, pr, lane, wr, s, hrow, gsv, pre);
+                stance = stance_reduce<SOLVE>(a, rb, P, pr, lane, wr, s, hrow, gsv, pre);
         }
         const bool fact = stance || !a.modes;
         if (fact) {
             if (!stance) slot_hessian_row(P, kap, pr, lane, hrow, gsv);
             const bool ok = factor12<SUB>(hrow, gsv, lane, s.ps.L, s.ps.ild, s.ps.xs);
             const double (&Mi)[12][12] = *reinterpret_cast<const double(*)[12][12]>(&s.ps.L[0][0]);
+            if constexpr (SOLVE && SUB == 16) {
+                if (stance && ok) {
+                    UST(a, rb, 11);
+                    solve_stance16(a, rb, lane, wr, P, s);
+                    return true;
+                }
+            }
             if (wr) {
                 for (int k = lane; k < 78; k += SUB) {
                     const int i = (int)((sqrt(8.0 * k + 1.0) - 1.0) * 0.5);
@@ -2771,7 +3139,11 @@ WBC_KERNEL_ATTR void wbc_step_kernel(KernelArgs a) {
     STAMP(a, rb, 6);
 }
 
-WBC_UPDATE_KERNEL_ATTR void wbc_update_kernel(KernelArgs a) {
+// The update kernel, and (SOLVE) its form that also solves the four-contact stance QPs whose
+// elimination succeeded (wbc_update_solve_kernel: stateless all-stance steps; the problem of such
+// a robot never goes to HBM, only its outputs do).
+template <bool SOLVE>
+__device__ __forceinline__ void update_kernel_body(const KernelArgs& a) {
     __shared__ UpdLds L;
     int seg, lane, rb;
     if constexpr (UPD_SUB == 64) {
@@ -2792,10 +3164,10 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_kernel(KernelArgs a) {
     // work row: [Prob | Presolve]; the Presolve record is stored by update_phase itself
     Presolve* pre = reinterpret_cast<Presolve*>(a.work + (size_t)rb * WORK_LEN + PROB_LEN);
     if (a.elim && blockIdx.x == 0 && threadIdx.x == 0) a.fb[a.parity ^ 1] = 0;  // for the next update
-    const bool stance = update_phase<UPD_SUB>(a, rb, lane, wr, L.u[seg], L.prob[seg], pre, L.model);
+    const bool stance = update_phase<UPD_SUB, SOLVE>(a, rb, lane, wr, L.u[seg], L.prob[seg], pre, L.model);
     const double2* src = reinterpret_cast<const double2*>(&L.prob[seg]);
     double2* dst = reinterpret_cast<double2*>(a.work + (size_t)rb * WORK_LEN);
-    if (wr) {
+    if (wr && !(SOLVE && stance)) {
         for (int k = lane; k < PROB_LEN / 2; k += UPD_SUB) dst[k] = src[k];
     }
     // mask-15 QPs whose elimination failed go to the fallback list (rare: one atomic each)
@@ -2809,6 +3181,8 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_kernel(KernelArgs a) {
         }
     }
 }
+WBC_UPDATE_KERNEL_ATTR void wbc_update_kernel(KernelArgs a) { update_kernel_body<false>(a); }
+WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) { update_kernel_body<WBC_STANCE_ELIM != 0>(a); }
 
 // Four-contact QP whose equalities the update kernel eliminated (its Presolve::stance flag, in
 // the record registers): wbc_solve_stance_kernel's; every other QP is wbc_solve_kernel's.
@@ -2943,6 +3317,15 @@ extern "C" hipError_t wbc_launch_solve_stance(const wbc::KernelArgs* a, hipStrea
     hipLaunchKernelGGL(wbc::wbc_solve_stance_kernel, dim3(a->batch), dim3(64), 0, st, *a);
     if (!WBC_AB_NO_FALLBACK)  // A/B measurement builds only (-DWBC_AB_NO_FALLBACK=1): not a correct solve
         hipLaunchKernelGGL(wbc::wbc_solve_fallback_kernel, dim3(16), dim3(64), 0, st, *a);
+    return hipGetLastError();
+}
+// Stateless all-stance step in two launches: the update kernel solving the stance QPs inline,
+// then the fallback kernel for the QPs whose elimination failed.
+extern "C" hipError_t wbc_launch_update_solve(const wbc::KernelArgs* a, hipStream_t st) {
+    if (!WBC_STANCE_ELIM || !a->elim || a->stateful || a->modes) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(wbc::wbc_update_solve_kernel, dim3((a->batch + wbc::UPD_RPW - 1) / wbc::UPD_RPW), dim3(64), 0,
+                       st, *a);
+    hipLaunchKernelGGL(wbc::wbc_solve_fallback_kernel, dim3(16), dim3(64), 0, st, *a);
     return hipGetLastError();
 }
 extern "C" hipError_t wbc_launch_reset(double* hist, const uint8_t* mask, int batch, hipStream_t st) {

@@ -11,7 +11,7 @@ OUT=gpurun_out/pmc_$TAG
 mkdir -p $OUT
 CMD="python3 bench.py --config $CONFIG --steps 10 --warmup 2 --no-cpu-baseline"
 case $CONFIG in
-  stance_*) STEPK=wbc_update_kernel,wbc_solve_stance_kernel,wbc_solve_fallback_kernel ;;
+  stance_*) STEPK=wbc_update_solve_kernel,wbc_solve_fallback_kernel ;;
   *) STEPK=wbc_update_kernel,wbc_solve_kernel ;;
 esac
 i=0
