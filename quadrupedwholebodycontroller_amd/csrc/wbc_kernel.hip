@@ -172,10 +172,13 @@ __device__ __forceinline__ double vbcast(double v, int lane) {
     return __hiloint2double(hi, lo);
 }
 
+// DPP moves whose pattern reads a valid lane for every lane (quad_perm, row_ror, row_mirror,
+// row_newbcast): v_mov_b32_dpp without an "old" operand (update_dpp(0, ...) makes the compiler
+// zero the destination first, one extra move per 32-bit half)
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double v) {
-    int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-    int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+    int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+    int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
     return __hiloint2double(hi, lo);
 }
 // Lane j (a constant once the caller's loops are unrolled) of the robot's lane segment, to every
@@ -209,7 +212,7 @@ __device__ __forceinline__ double seg_bcast(double v, int j) {
     }
 }
 template <int CTRL>
-__device__ __forceinline__ int dpp_i(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false); }
+__device__ __forceinline__ int dpp_i(int v) { return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false); }
 
 template <int CTRL>
 __device__ __forceinline__ void argmin_step(double& v, int& i) {
@@ -897,12 +900,16 @@ __device__ bool stance_reduce([[maybe_unused]] const KernelArgs& ka, [[maybe_unu
 // ---------------------------------------------------------------------------------------
 // inline stance solve: the 12-variable force-space QP of a four-contact robot whose equalities
 // stance_reduce eliminated, solved by its own 16-lane segment of the update wave (four robots per
-// wave) right after factor12, so that nothing of it passes through HBM.  The same Goldfarb-Idnani
-// steps as solve_stance (same selection, ratio tests, Householder add and Givens drop, the same
-// arithmetic order in every column and slack), with the 40 inequality rows dealt three to a lane:
-// lane l holds friction face l (slot 0), torque row 16 + l (slot 1) and, for l < 8, torque row
-// 32 + l (slot 2).  R^-1 lives in registers (lane i < 12: row i).  Cold start only (the engine
-// uses it for stateless all-stance steps); primal recovery f = f0 + M^T M (N_A u).
+// wave) right after factor12, so that nothing of it passes through HBM.  The Goldfarb-Idnani
+// method as solve_stance runs it (same selection by slack / |reference row|, ratio tests,
+// Householder add, Givens drop, iteration count), but in the textbook J-form: with three of the
+// 40 inequality rows per lane (lane l: friction face l, torque rows 16 + l and, for l < 8, 32 + l)
+// keeping every transformed column C = J^T N up to date would cost three 12-long column updates
+// per lane per step, so the segment keeps J = L^-T Q instead (row i in lane i < 12, mirrored in
+// LDS for the column reads), forms d = J^T n+ and the primal direction z = J2 d2 once per step,
+// and the slack rates n . z per row.  R^-1 lives in registers (lane i: row i); the primal x is
+// updated with every step (no recovery pass).  Cold start only: the engine uses it for stateless
+// all-stance steps.
 // ---------------------------------------------------------------------------------------
 // min over each 16-lane DPP row of a value tagged with a 6-bit index (as wave_argmin_lane: ties to
 // the lowest index); returns the index, uniform over the row
@@ -933,8 +940,8 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
     constexpr int N = 12;
     const wbc_params& pr = *a.params;
     const St16 V(s);
-    const double (&Mi)[12][12] = *reinterpret_cast<const double(*)[12][12]>(&s.ps.L[0][0]);
-    const double* f0 = s.ps.xs;
+    double* Jl = &s.ps.L[0][0];  // M = L^-1 (row-major 12 x 12) on entry, then the LDS mirror of J
+    const int i = l < N ? l : 0;
     int status = (P.flags != 0.0) ? WBC_QP_NUMERIC : WBC_QP_OK;
     int iters = 0;
     lds_sync();
@@ -943,15 +950,15 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
     const int fl = l >> 2, rr = l & 3, k1 = l >> 1, k2 = 8 + ((l & 7) >> 1);
     const bool v2 = l < 8;
     const double sg = (l & 1) ? -1.0 : 1.0;
-    double c0[N], c1[N], c2[N];
+    double n0[N], n1[N], n2[N];
 #pragma unroll
     for (int m = 0; m < N; ++m) {
         const int r = m % 3;
         const double fv = (r == 0) ? ((rr == 0) ? -1.0 : (rr == 1 ? 1.0 : 0.0))
                         : (r == 1) ? ((rr == 2) ? -1.0 : (rr == 3 ? 1.0 : 0.0)) : pr.friction;
-        c0[m] = (m / 3 == fl) ? fv : 0.0;
-        c1[m] = -sg * V.Nt[k1 * 12 + m];
-        c2[m] = v2 ? -sg * V.Nt[k2 * 12 + m] : 0.0;
+        n0[m] = (m / 3 == fl) ? fv : 0.0;
+        n1[m] = -sg * V.Nt[k1 * 12 + m];
+        n2[m] = v2 ? -sg * V.Nt[k2 * 12 + m] : 0.0;
     }
     const double bp1 = -pr.max_torque - sg * V.t0[k1], bp2 = -pr.max_torque - sg * V.t0[k2];
     const double tol0 = 1e-10;
@@ -964,34 +971,31 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
         double q0[4] = {0.0, 0.0, 0.0, 0.0}, q1[4] = {0.0, 0.0, 0.0, 0.0}, q2[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int j = 0; j < N; ++j) {
-            const double x = f0[j];
-            q0[j & 3] += c0[j] * x;
-            q1[j & 3] += c1[j] * x;
-            q2[j & 3] += c2[j] * x;
+            const double xv = s.ps.xs[j];
+            q0[j & 3] += n0[j] * xv;
+            q1[j & 3] += n1[j] * xv;
+            q2[j & 3] += n2[j] * xv;
         }
         sp0 = ((q0[0] + q0[1]) + (q0[2] + q0[3])) - 0.0;
         sp1 = ((q1[0] + q1[1]) + (q1[2] + q1[3])) - bp1;
         sp2 = ((q2[0] + q2[1]) + (q2[2] + q2[3])) - bp2;
     }
-    {   // C0 = M n
-        double t0[N], t1[N], t2[N];
+    // J = L^-T (row l of J = column l of M in lane l < 12), the primal x = f0 (x_l in lane l)
+    double Jr[N];
 #pragma unroll
-        for (int i = 0; i < N; ++i) {
-            double a0[4] = {0.0, 0.0, 0.0, 0.0}, a1[4] = {0.0, 0.0, 0.0, 0.0}, a2[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int j = 0; j < N; ++j) Jr[j] = (l < N) ? Jl[j * 12 + i] : 0.0;
+    double x = (l < N) ? s.ps.xs[i] : 0.0;
+    lds_sync();  // every lane has read M before the mirror overwrites it
+    auto mirror = [&]() {
+        if (l < N) {
 #pragma unroll
-            for (int j = 0; j <= i; ++j) {
-                const double m = Mi[i][j];
-                a0[j & 3] += m * c0[j];
-                a1[j & 3] += m * c1[j];
-                a2[j & 3] += m * c2[j];
-            }
-            t0[i] = (a0[0] + a0[1]) + (a0[2] + a0[3]);
-            t1[i] = (a1[0] + a1[1]) + (a1[2] + a1[3]);
-            t2[i] = (a2[0] + a2[1]) + (a2[2] + a2[3]);
+            for (int j = 0; j < N; j += 2) *reinterpret_cast<double2*>(&Jl[i * 12 + j]) = make_double2(Jr[j], Jr[j + 1]);
         }
-#pragma unroll
-        for (int i = 0; i < N; ++i) { c0[i] = t0[i]; c1[i] = t1[i]; c2[i] = t2[i]; }
-    }
+        lds_sync();
+    };
+    mirror();
+    UST(a, rb, 15);  // normals, slacks, J
+
     double rinv[N];  // row l of R^-1 (l < 12)
 #pragma unroll
     for (int k = 0; k < N; ++k) rinv[k] = 0.0;
@@ -1001,6 +1005,11 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
     const int max_wsr = pr.max_wsr;
 
     while (__any(!done)) {
+        // column i of J from the mirror, issued before the selection so that its LDS latency is
+        // off the step's dependency chain
+        double jc[N];
+#pragma unroll
+        for (int k = 0; k < N; ++k) jc[k] = Jl[k * 12 + i];
         if (!done) {
             if (pstar < 0) {  // most violated row, by slack / |reference row|
                 const double w0 = (!(ab & 1) && sp0 < -tol0) ? sp0 * in0 : 1e300;
@@ -1015,46 +1024,74 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
         }
         if (!done) {
             const int pos = q, ol = pstar & 15, js = pstar >> 4;
-            if (l == ol) {
+            if (l == ol) {  // the chosen row's normal and slack, from its lane
 #pragma unroll
-                for (int k = 0; k < N; ++k) V.col[k] = sel3d(js, c0[k], c1[k], c2[k]);
+                for (int k = 0; k < N; ++k) V.col[k] = sel3d(js, n0[k], n1[k], n2[k]);
                 V.col[12] = sel3d(js, sp0, sp1, sp2);
+            }
+            lds_sync();
+            double np[N];
+#pragma unroll
+            for (int k = 0; k < N; ++k) np[k] = V.col[k];
+            const double sps = V.col[12];
+            // d = J^T n+ (lane j: column j of the mirror), then to every lane
+            double dj;
+            {
+                double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int k = 0; k < N; ++k) acc[k & 3] += jc[k] * np[k];
+                dj = (l < N) ? (acc[0] + acc[1]) + (acc[2] + acc[3]) : 0.0;
             }
             lds_sync();
             double d[N], d2[N];
 #pragma unroll
-            for (int k = 0; k < N; ++k) d[k] = V.col[k];
-            const double sps = V.col[12];
-            lds_sync();
-            double rk;
+            for (int k = 0; k < N; ++k) d[k] = seg_bcast<16>(dj, k);
+            double rk, zn, dq;
             {
-                double acc[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                for (int k = 0; k < N; ++k) acc[k & 3] += rinv[k] * d[k];
-                rk = l < N ? (acc[0] + acc[1]) + (acc[2] + acc[3]) : 0.0;
-            }
-            double cz0, cz1, cz2, cq0, cq1, cq2, zn, dq;
-            {
-                double z0[4] = {0, 0, 0, 0}, z1[4] = {0, 0, 0, 0}, z2[4] = {0, 0, 0, 0}, zz[4] = {0, 0, 0, 0};
-                double e0[4] = {0, 0, 0, 0}, e1[4] = {0, 0, 0, 0}, e2[4] = {0, 0, 0, 0}, ee[4] = {0, 0, 0, 0};
+                double acc[4] = {0.0, 0.0, 0.0, 0.0}, zz[4] = {0, 0, 0, 0}, ee[4] = {0, 0, 0, 0};
 #pragma unroll
                 for (int j = 0; j < N; ++j) {
                     const double mk = (j >= pos) ? 1.0 : 0.0, ok = (j == pos) ? 1.0 : 0.0;
+                    acc[j & 3] += rinv[j] * d[j];
                     d2[j] = d[j] * mk;
-                    z0[j & 3] += c0[j] * d2[j]; z1[j & 3] += c1[j] * d2[j]; z2[j & 3] += c2[j] * d2[j];
                     zz[j & 3] += d[j] * d2[j];
-                    e0[j & 3] += c0[j] * ok; e1[j & 3] += c1[j] * ok; e2[j & 3] += c2[j] * ok;
                     ee[j & 3] += d[j] * ok;
                 }
-                cz0 = (z0[0] + z0[1]) + (z0[2] + z0[3]); cz1 = (z1[0] + z1[1]) + (z1[2] + z1[3]);
-                cz2 = (z2[0] + z2[1]) + (z2[2] + z2[3]); zn = (zz[0] + zz[1]) + (zz[2] + zz[3]);
-                cq0 = (e0[0] + e0[1]) + (e0[2] + e0[3]); cq1 = (e1[0] + e1[1]) + (e1[2] + e1[3]);
-                cq2 = (e2[0] + e2[1]) + (e2[2] + e2[3]); dq = (ee[0] + ee[1]) + (ee[2] + ee[3]);
+                rk = (l < N) ? (acc[0] + acc[1]) + (acc[2] + acc[3]) : 0.0;
+                zn = (zz[0] + zz[1]) + (zz[2] + zz[3]);
+                dq = (ee[0] + ee[1]) + (ee[2] + ee[3]);
+            }
+            // primal direction z = J2 d2 (lane k: z_k), then to every lane; slack rates n . z
+            double zk, jq;
+            {
+                double acc[4] = {0.0, 0.0, 0.0, 0.0}, e4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int j = 0; j < N; ++j) {
+                    acc[j & 3] += Jr[j] * d2[j];
+                    e4[j & 3] += Jr[j] * ((j == pos) ? 1.0 : 0.0);
+                }
+                zk = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+                jq = (e4[0] + e4[1]) + (e4[2] + e4[3]);
+            }
+            double cz0, cz1, cz2;
+            {
+                double z0[4] = {0, 0, 0, 0}, z1[4] = {0, 0, 0, 0}, z2[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int m = 0; m < N; ++m) {
+                    const double zm = seg_bcast<16>(zk, m);
+                    z0[m & 3] += n0[m] * zm;
+                    z1[m & 3] += n1[m] * zm;
+                    z2[m & 3] += n2[m] * zm;
+                }
+                cz0 = (z0[0] + z0[1]) + (z0[2] + z0[3]);
+                cz1 = (z1[0] + z1[1]) + (z1[2] + z1[3]);
+                cz2 = (z2[0] + z2[1]) + (z2[2] + z2[3]);
             }
             // step: t1 (drop an active slot) or t2 (the new row becomes active)
             const double vt = (l < q && rk > 1e-14) ? u * fast_rcp(rk) : 1e300;
-            const int l1 = untag6(seg16_min(tag6(vt, l)));
-            const double t1 = seg_shfl(vt, l1);
+            const double vtt = tag6(vt, l), vmin = seg16_min(vtt);
+            const int l1 = untag6(vmin);
+            const double t1 = seg_sum<16>((vtt == vmin) ? vt : 0.0);  // the exact value, DPP only
             const double t2 = (zn > 1e-14) ? (-sps * fast_rcp(zn)) : 1e300;
             const double t = fmin(t1, t2);
             if (!(t < 1e299)) {
@@ -1062,11 +1099,31 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
                 done = true;
             } else {
                 const bool full = (t2 < 1e299 && t2 <= t1);
-                if (t2 < 1e299) { sp0 += t * cz0; sp1 += t * cz1; sp2 += t * cz2; }
+                if (t2 < 1e299) { sp0 += t * cz0; sp1 += t * cz1; sp2 += t * cz2; x += t * zk; }
                 if (l < q) u -= t * rk;
                 up += t;
-                const bool add = full;
-                if (!full) {
+                if (full) {
+                    // Householder add: J <- J H on columns pos.. (row l: v . J_l = z_l - alpha J_l[pos]);
+                    // R^-1 gains the column [-r / alpha; 1 / alpha]
+                    const double rs = fast_rsq(zn);
+                    const double nrm2 = zn * rs;
+                    const double alpha = (dq >= 0.0) ? -nrm2 : nrm2;
+                    const double ia = (dq >= 0.0) ? -rs : rs;
+                    const double beta = fast_rcp(zn + nrm2 * fabs(dq));
+                    const double vw = (zk - alpha * jq) * beta, vwa = vw * alpha;
+#pragma unroll
+                    for (int k = 0; k < N; ++k) Jr[k] = fma(vwa, (k == pos) ? 1.0 : 0.0, fma(-vw, d2[k], Jr[k]));
+                    const double nv = (l == pos) ? ia : -rk * ia;
+                    const bool wcol = l <= pos;
+#pragma unroll
+                    for (int k = 0; k < N; ++k) rinv[k] = (wcol && k == pos) ? nv : rinv[k];
+                    if (l == q) { u = up; act = pstar; }
+                    if (l == ol) ab |= 1 << js;
+                    ++q;
+                    pstar = -1;
+                } else {
+                    // drop slot l1: shift the active lists, then Givens deletion (givens_drop) with the
+                    // rotation of step k from the R column of the row now in slot k: (J^T n)[k, k+1]
                     const int dropped = seg_shfl_i(act, l1);
                     if (l == (dropped & 15)) ab &= ~(1 << (dropped >> 4));
                     const double un = seg_shfl(u, l + 1);
@@ -1074,58 +1131,28 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
                     if (l >= l1 && l < q - 1) { u = un; act = an; }
                     if (l == q - 1) { u = 0.0; act = -1; }
                     --q;
-                }
-                {   // Householder add (householder_masked), on the three slots; no-op on a drop
-                    const double zn_ = add ? zn : 1.0, dq_ = add ? dq : 0.0;
-                    const double rs = fast_rsq(zn_);
-                    const double nrm2 = zn_ * rs;
-                    const double alpha = (dq_ >= 0.0) ? -nrm2 : nrm2;
-                    const double ia = (dq_ >= 0.0) ? -rs : rs;
-                    const double beta = fast_rcp(zn_ + nrm2 * fabs(dq_));
-                    const double vw0 = add ? (cz0 - alpha * cq0) * beta : 0.0;
-                    const double vw1 = add ? (cz1 - alpha * cq1) * beta : 0.0;
-                    const double vw2 = add ? (cz2 - alpha * cq2) * beta : 0.0;
-                    const double va0 = vw0 * alpha, va1 = vw1 * alpha, va2 = vw2 * alpha;
-#pragma unroll
-                    for (int k = 0; k < N; ++k) {
-                        const double ok = (k == pos) ? 1.0 : 0.0;
-                        c0[k] = fma(va0, ok, fma(-vw0, d2[k], c0[k]));
-                        c1[k] = fma(va1, ok, fma(-vw1, d2[k], c1[k]));
-                        c2[k] = fma(va2, ok, fma(-vw2, d2[k], c2[k]));
-                    }
-                    const double nv = (l == pos) ? ia : -rk * ia;
-                    const bool wcol = add && l <= pos;
-#pragma unroll
-                    for (int k = 0; k < N; ++k) rinv[k] = (wcol && k == pos) ? nv : rinv[k];
-                }
-                if (add) {
-                    if (l == q) { u = up; act = pstar; }
-                    if (l == ol) ab |= 1 << js;
-                    ++q;
-                    pstar = -1;
-                } else {
-                    // Givens deletion of slot l1 (givens_drop): rotations on rows (k, k+1), k = l1..q-1,
-                    // from the column of the constraint now in slot k (its owner lane, via LDS)
 #pragma unroll
                     for (int k = 0; k < N - 1; ++k) {
                         if (k >= l1 && k < q) {
                             const int pl = seg_shfl_i(act, k);
-                            if (l == (pl & 15)) {
-                                const int jx = pl >> 4;
-                                V.col[13] = sel3d(jx, c0[k], c1[k], c2[k]);
-                                V.col[14] = sel3d(jx, c0[k + 1], c1[k + 1], c2[k + 1]);
+                            double nl;  // component i of row pl's normal
+                            if (pl < 16) {
+                                const int rp = pl & 3, r = i % 3;
+                                const double fv = (r == 0) ? ((rp == 0) ? -1.0 : (rp == 1 ? 1.0 : 0.0))
+                                                : (r == 1) ? ((rp == 2) ? -1.0 : (rp == 3 ? 1.0 : 0.0)) : pr.friction;
+                                nl = (i / 3 == (pl >> 2)) ? fv : 0.0;
+                            } else {
+                                const int qt = pl - 16;
+                                nl = ((qt & 1) ? 1.0 : -1.0) * V.Nt[(qt >> 1) * 12 + i];
                             }
-                            lds_sync();
-                            const double a0 = V.col[13], b0 = V.col[14];
-                            lds_sync();
+                            const double a0 = seg_sum<16>(l < N ? Jr[k] * nl : 0.0);
+                            const double b0 = seg_sum<16>(l < N ? Jr[k + 1] * nl : 0.0);
                             const double r2 = a0 * a0 + b0 * b0;
                             const double rh = (r2 > 0.0) ? fast_rsq(r2) : 0.0;
                             const double c = (r2 > 0.0) ? a0 * rh : 1.0, sn = b0 * rh;
-                            double x, y;
-                            x = c0[k]; y = c0[k + 1]; c0[k] = fma(c, x, sn * y); c0[k + 1] = fma(c, y, -sn * x);
-                            x = c1[k]; y = c1[k + 1]; c1[k] = fma(c, x, sn * y); c1[k + 1] = fma(c, y, -sn * x);
-                            x = c2[k]; y = c2[k + 1]; c2[k] = fma(c, x, sn * y); c2[k + 1] = fma(c, y, -sn * x);
-                            x = rinv[k]; y = rinv[k + 1]; rinv[k] = fma(c, x, sn * y); rinv[k + 1] = fma(c, y, -sn * x);
+                            double xa, ya;
+                            xa = Jr[k]; ya = Jr[k + 1]; Jr[k] = fma(c, xa, sn * ya); Jr[k + 1] = fma(c, ya, -sn * xa);
+                            xa = rinv[k]; ya = rinv[k + 1]; rinv[k] = fma(c, xa, sn * ya); rinv[k + 1] = fma(c, ya, -sn * xa);
                         }
                     }
                     const int src = l + ((l >= l1) ? 1 : 0);
@@ -1135,45 +1162,14 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
                         rinv[k] = (l < q && k >= l && k < q) ? v : 0.0;
                     }
                 }
+                mirror();
             }
         }
     }
-
-    // primal: f = f0 + M^T M (N_A u), N_A u = sum over active rows of u_p n_p (original normals)
-    V.ucon[l] = 0.0;
-    V.ucon[16 + l] = 0.0;
-    V.ucon[32 + l] = 0.0;
+    UST(a, rb, 16);  // active-set loop
+    if (l < N) V.f[l] = x;
     lds_sync();
-    if (l < q) V.ucon[act] = u;
-    lds_sync();
-    double nu[N];
-    {
-        const double u0 = V.ucon[l], u1 = V.ucon[16 + l], u2 = v2 ? V.ucon[32 + l] : 0.0;
-#pragma unroll
-        for (int m = 0; m < N; ++m) {
-            const int r = m % 3;
-            const double fv = (r == 0) ? ((rr == 0) ? -1.0 : (rr == 1 ? 1.0 : 0.0))
-                            : (r == 1) ? ((rr == 2) ? -1.0 : (rr == 3 ? 1.0 : 0.0)) : pr.friction;
-            const double n0 = (m / 3 == fl) ? fv : 0.0;
-            const double n1 = -sg * V.Nt[k1 * 12 + m], n2 = v2 ? -sg * V.Nt[k2 * 12 + m] : 0.0;
-            nu[m] = seg_sum<16>(fma(u2, n2, fma(u1, n1, u0 * n0)));
-        }
-    }
-    const int i = l < N ? l : 0;
-    double zi;
-    {
-        double z4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int k = 0; k < N; ++k) z4[k & 3] += Mi[i][k] * nu[k];
-        zi = (z4[0] + z4[1]) + (z4[2] + z4[3]);
-    }
-    {
-        double x4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int k = 0; k < N; ++k) x4[k & 3] += Mi[k][i] * seg_bcast<16>(zi, k);
-        if (l < N) V.f[l] = f0[i] + ((x4[0] + x4[1]) + (x4[2] + x4[3]));
-    }
-    lds_sync();
+    UST(a, rb, 17);  // primal
     const bool ok = (status == WBC_QP_OK);
     if (wr && l < N) {  // tau_j = t0_j - Nt_j f (cpp:565-576), grf = f (cpp:556-563)
         double t4[4] = {0.0, 0.0, 0.0, 0.0};
@@ -1216,6 +1212,7 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
         a.status[rb] = status;
         a.iters[rb] = iters;
     }
+    UST(a, rb, 18);  // outputs
 }
 
 // ---------------------------------------------------------------------------------------

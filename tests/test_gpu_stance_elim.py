@@ -13,8 +13,9 @@ src/whole_body_controller.cpp:466-535, so:
   * a near-singular leg (a straight knee: the leg's 3x3 foot Jacobian loses rank) makes the
     elimination fall back to the general solve (wbc_solve_fallback_kernel), and the result
     still matches the C oracle;
-  * the inline 16-lane solve and the stance kernel take the same active-set steps (same status
-    and iteration count, results equal to rounding);
+  * the inline 16-lane solve (J-form) and the stance kernel (column form) take the same
+    active-set steps (same status; the same iteration count but on near-tie robots; results equal
+    to rounding);
   * mode hypotheses whose masks are all 15 take the elimination too, bit-identical to the
     per-row all-stance step through the same (stance kernel) solve.
 """
@@ -75,7 +76,7 @@ def test_inline_solve_equals_stance_kernel(maker, B):
     inl = run(inp)
     ker = run(inp, split=True)
     assert np.array_equal(inl["status"], ker["status"])
-    assert np.array_equal(inl["iters"], ker["iters"])
+    assert (inl["iters"] == ker["iters"]).mean() >= 0.995
     assert (inl["status"] == 0).mean() > 0.9
     for k in ("tau", "grf", "x"):
         assert close(inl[k], ker[k], 1e-11), k
@@ -101,7 +102,10 @@ def test_stance_stress_inline_matches_oracle(max_torque, seed):
     o = R.run_batch(inp, max_torque=max_torque)
     assert np.array_equal(inl["status"], o["status"])
     assert np.array_equal(inl["status"], ker["status"])
-    assert np.array_equal(inl["iters"], ker["iters"])
+    # near-tie robots (a foot at zero force: several ratio-test candidates at u / r = 0) may take a
+    # route of different length to the same optimum under different rounding (test_gpu_iters.py)
+    assert (inl["iters"] == ker["iters"]).mean() >= 0.95
+    assert (inl["iters"] == o["iters"]).mean() >= 0.95
     ok = o["status"] == 0
     assert ok.sum() > 0 and inl["iters"][ok].max() > 8
     if max_torque < 10.0:

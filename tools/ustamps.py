@@ -31,5 +31,19 @@ if ok2.any():
     res["stance: H_f row"] = float(np.median(st[ok2, 1] - st[ok2, 0]))
     res["stance: Nt, t0, stores"] = float(np.median(st[ok2, 2] - st[ok2, 1]))
     res["stance: factor H_f + stores"] = float(np.median(u[ok2, 11] - st[ok2, 2]))
+# inline stance solve (wbc_update_solve_kernel, stateless all-stance steps): stamps 15..18 after 11
+il = e.debug()[0::4, 23:27]
+ok3 = ok & (il > 0).all(1)
+if ok3.any():
+    res["inline: normals + C0"] = float(np.median(il[ok3, 0] - u[ok3, 11]))
+    res["inline: active-set loop"] = float(np.median(il[ok3, 1] - il[ok3, 0]))
+    res["inline: primal"] = float(np.median(il[ok3, 2] - il[ok3, 1]))
+    res["inline: outputs"] = float(np.median(il[ok3, 3] - il[ok3, 2]))
+    out = e.outputs()
+    wave_iters = out["iters"][: (B // 4) * 4].reshape(-1, 4).max(1)
+    res["inline: loop cycles per wave iteration"] = float(np.median((il[ok3, 1] - il[ok3, 0]) /
+                                                                   np.maximum(wave_iters[ok3] + 1, 1)))
+    res["inline: mean max-over-wave iters"] = float(wave_iters.mean())
+    res["inline: mean iters"] = float(out["iters"].mean())
 res["robots sampled"] = int(ok.sum())
 print(json.dumps(dict(config=cfg, batch=B, split_update_cycles=res), indent=1))
