@@ -911,6 +911,9 @@ __device__ bool stance_reduce([[maybe_unused]] const KernelArgs& ka, [[maybe_unu
 // updated with every step (no recovery pass).  Cold start only: the engine uses it for stateless
 // all-stance steps.
 // ---------------------------------------------------------------------------------------
+#ifndef WBC_NPLUS_DIRECT
+#define WBC_NPLUS_DIRECT 0  // 1 measured slower: B = 4096 stance 88.0 -> 80.3 M solves/s (profiles/r02/s/var_np.log)
+#endif
 // min over each 16-lane DPP row of a value tagged with a 6-bit index (as wave_argmin_lane: ties to
 // the lowest index); returns the index, uniform over the row
 __device__ __forceinline__ double tag6(double v, int idx) {
@@ -1024,6 +1027,24 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
         }
         if (!done) {
             const int pos = q, ol = pstar & 15, js = pstar >> 4;
+#if WBC_NPLUS_DIRECT
+            // the chosen row's normal n+ (friction pattern, or +- a row of Nt), formed by every
+            // lane; its slack from its lane by a DPP sum (no LDS round trip on the chain)
+            double np[N];
+            {
+                const bool isf = pstar < 16;
+                const int pl = pstar >> 2, rp = pstar & 3, qt = isf ? 0 : pstar - 16;
+                const double sgn = (qt & 1) ? 1.0 : -1.0;
+                const double fr0 = (rp == 0) ? -1.0 : (rp == 1 ? 1.0 : 0.0), fr1 = (rp == 2) ? -1.0 : (rp == 3 ? 1.0 : 0.0);
+                const double* nt = V.Nt + (qt >> 1) * 12;
+#pragma unroll
+                for (int m = 0; m < N; ++m) {
+                    const double fv = (m % 3 == 0) ? fr0 : (m % 3 == 1) ? fr1 : pr.friction;
+                    np[m] = isf ? ((m / 3 == pl) ? fv : 0.0) : sgn * nt[m];
+                }
+            }
+            const double sps = seg_sum<16>((l == ol) ? sel3d(js, sp0, sp1, sp2) : 0.0);
+#else
             if (l == ol) {  // the chosen row's normal and slack, from its lane
 #pragma unroll
                 for (int k = 0; k < N; ++k) V.col[k] = sel3d(js, n0[k], n1[k], n2[k]);
@@ -1034,6 +1055,7 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
 #pragma unroll
             for (int k = 0; k < N; ++k) np[k] = V.col[k];
             const double sps = V.col[12];
+#endif
             // d = J^T n+ (lane j: column j of the mirror), then to every lane
             double dj;
             {
