@@ -684,19 +684,31 @@ __device__ bool stance_reduce([[maybe_unused]] const KernelArgs& ka, [[maybe_unu
         R.w[i] = wi;
     }
     lds_sync();
-    // [S | z] = [I - K W | K w], K[a][j] = A_j[a] / m (a < 3), (I_c^-1 A_ang)_j[a - 3]: 42 entries
-    for (int t = lane; t < 42; t += 16) {
-        const int ra = t / 7, cb = t % 7;
-        double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    UST(ka, rb, 19);  // leg inverses, W rows
+    // [S | z] = [I - K W | K w], K[a][j] = A_j[a] / m (a < 3), (I_c^-1 A_ang)_j[a - 3]: 42 entries in
+    // one round, lane < 12 -> row lane % 6, columns 0..2 or 3..6 (h = lane / 6), each entry summed
+    // in the same order as a one-entry-per-lane loop
+    {
+        const int ra = lane % 6, h = (lane / 6) & 1;
+        double acc[4][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
 #pragma unroll
         for (int j = 0; j < 12; ++j) {
-            const double kj = (ra < 3) ? s.A[j][ra] * inv_m : s.KA[j][ra - 3];
-            acc[j & 3] = fma(kj, (cb < 6) ? R.W[j][cb] : R.w[j], acc[j & 3]);
+            const double kj = (ra < 3) ? s.A[j][ra] * inv_m : s.KA[j][ra < 3 ? 0 : ra - 3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) acc[c][j & 3] = fma(kj, R.W[j][3 * h + c], acc[c][j & 3]);
+            acc[3][j & 3] = fma(kj, R.w[j], acc[3][j & 3]);
         }
-        const double v = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-        R.S[ra][cb] = (cb < 6) ? ((ra == cb ? 1.0 : 0.0) - v) : v;
+        if (lane < 12) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const int cb = 3 * h + c;
+                R.S[ra][cb] = (ra == cb ? 1.0 : 0.0) - ((acc[c][0] + acc[c][1]) + (acc[c][2] + acc[c][3]));
+            }
+            if (h) R.S[ra][6] = (acc[3][0] + acc[3][1]) + (acc[3][2] + acc[3][3]);
+        }
     }
     lds_sync();
+    UST(ka, rb, 20);  // S
     // S^-1 by Gauss-Jordan without pivoting (S is well conditioned: cond < 10 on the bench and
     // stress states, smallest pivot > 0.25 max|S|; a pivot below 1e-6 max|S| takes the general
     // path), row r in lane r < 6, pivot rows broadcast with DPP row_newbcast
@@ -763,15 +775,26 @@ __device__ bool stance_reduce([[maybe_unused]] const KernelArgs& ka, [[maybe_unu
         }
     }
     lds_sync();
-    // [Q | v] = [Y^T Y | Y^T q0]: 42 entries
-    for (int t = lane; t < 42; t += 16) {
-        const int ra = t / 7, cb = t % 7;
-        double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    UST(ka, rb, 21);  // Y, q0
+    // [Q | v] = [Y^T Y | Y^T q0]: 42 entries in one round, as S above
+    {
+        const int ra = lane % 6, h = (lane / 6) & 1;
+        double acc[4][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
 #pragma unroll
-        for (int j = 0; j < 12; ++j) acc[j & 3] = fma(R.Y[j][ra], (cb < 6) ? R.Y[j][cb] : R.q0[j], acc[j & 3]);
-        R.Q[ra][cb] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+        for (int j = 0; j < 12; ++j) {
+            const double yj = R.Y[j][ra];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) acc[c][j & 3] = fma(yj, R.Y[j][3 * h + c], acc[c][j & 3]);
+            acc[3][j & 3] = fma(yj, R.q0[j], acc[3][j & 3]);
+        }
+        if (lane < 12) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) R.Q[ra][3 * h + c] = (acc[c][0] + acc[c][1]) + (acc[c][2] + acc[c][3]);
+            if (h) R.Q[ra][6] = (acc[3][0] + acc[3][1]) + (acc[3][2] + acc[3][3]);
+        }
     }
     lds_sync();
+    UST(ka, rb, 22);  // Q = Y^T Y
     // H^ rows (lane a < 6) over S: H^ = I + Mb^-2 + Mb^-1 Q Mb^-1, Mb^-1 = diag(I / m, I_c^-1)
     {
         const int ra = lane < 6 ? lane : 5;

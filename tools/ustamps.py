@@ -26,6 +26,16 @@ res["total (stamps 0..11)"] = float(np.median(u[ok, -1] - u[ok, 0]))
 # four-contact stance stage inside the presolve slot (stamps 12..14, written before stamp 11)
 st = e.debug()[0::4, 20:23]
 ok2 = ok & (st > 0).all(1)
+s2 = e.debug()[0::4, 27:29]  # stamps 19, 20 inside the first stance stage
+if ok2.any() and (s2[ok2] > 0).all():
+    res["stance: leg inverses, W"] = float(np.median(s2[ok2, 0] - u[ok2, 10]))
+    res["stance: S = I - K W"] = float(np.median(s2[ok2, 1] - s2[ok2, 0]))
+    res["stance: S^-1 (Gauss-Jordan)"] = float(np.median(st[ok2, 0] - s2[ok2, 1]))
+s3 = e.debug()[0::4, 29:31]  # stamps 21, 22 inside the second stance stage
+if ok2.any() and (s3[ok2] > 0).all():
+    res["stance: Y, q0"] = float(np.median(s3[ok2, 0] - st[ok2, 0]))
+    res["stance: Q = Y^T Y"] = float(np.median(s3[ok2, 1] - s3[ok2, 0]))
+    res["stance: H^, H_f row, g_f"] = float(np.median(st[ok2, 1] - s3[ok2, 1]))
 if ok2.any():
     res["stance: Gauss-Jordan"] = float(np.median(st[ok2, 0] - u[ok2, 10]))
     res["stance: H_f row"] = float(np.median(st[ok2, 1] - st[ok2, 0]))
