@@ -342,6 +342,10 @@ __device__ __forceinline__ bool seg_any(bool p) {
 #ifndef WBC_STANCE_ELIM
 #define WBC_STANCE_ELIM 1
 #endif
+// Inline solve's force-space factor: 1 = rank-6 form (rank6_factor), 0 = 12 x 12 Cholesky (factor12)
+#ifndef WBC_RANK6
+#define WBC_RANK6 1
+#endif
 #ifndef WBC_STANCE_KERNEL
 #define WBC_STANCE_KERNEL 1  // 1: stance QPs in wbc_solve_stance_kernel (+ fallback kernel); 0: in wbc_solve_kernel
 #endif
@@ -432,6 +436,9 @@ __device__ __forceinline__ double fast_rsq(double x) {
     return fma(y, e, y);
 }
 __device__ __forceinline__ double sel3(const double* v, int k) { return k == 0 ? v[0] : (k == 1 ? v[1] : v[2]); }
+__device__ __forceinline__ double sel4d(int k, double a, double b, double c, double d) {
+    return k == 0 ? a : (k == 1 ? b : (k == 2 ? c : d));
+}
 
 // Diagnostic build only (-DWBC_STAMPS): lane 0 records the shader clock at phase boundaries into
 // the robot's debug record slots WBC_DBG_STAMPS.. (never read by the kernel, never an output).
@@ -542,7 +549,8 @@ __device__ __forceinline__ void slot_hessian_row(const Prob& P, int kap, const w
 // inverse M = L^-1 (lower, written over L) and x0 = -H^-1 g (g_i in lane i).  Returns false when
 // the matrix is not positive definite.
 template <int SUB>
-__device__ bool factor12(double (&hrow)[12], double gsv, int lane, double (&L)[12][13], double* ild, double* xs) {
+__device__ bool factor12(double (&hrow)[12], double gsv, int lane, double (&L)[12][13], double* ild, double* xs,
+                         [[maybe_unused]] const KernelArgs* ka = nullptr, [[maybe_unused]] int rb = 0) {
     // right-looking Cholesky, row i in lane i; L_jk broadcast from lane j of the segment
     bool chol_ok = true;
     double ildv = 1.0;  // lane k: 1 / L_kk
@@ -565,6 +573,7 @@ __device__ bool factor12(double (&hrow)[12], double gsv, int lane, double (&L)[1
         ild[lane] = ildv;
     }
     lds_sync();  // L visible
+    if (ka) UST(*ka, rb, 23);  // Cholesky
     // M = L^-1 (lower triangular), lane j forms column j by forward substitution; every later
     // use of the factor (C0 = L^-1 n_s, x0, primal recovery) is then a matvec without a chain
     double (&Mi)[12][12] = *reinterpret_cast<double(*)[12][12]>(&L[0][0]);
@@ -584,6 +593,7 @@ __device__ bool factor12(double (&hrow)[12], double gsv, int lane, double (&L)[1
         }
     }
     lds_sync();
+    if (ka) UST(*ka, rb, 24);  // M = L^-1
     // x0 = -H^-1 g = -M^T (M g): g_k and z_k broadcast from lane k
     {
         double gk[12];
@@ -838,7 +848,9 @@ __device__ bool stance_reduce([[maybe_unused]] const KernelArgs& ka, [[maybe_unu
     for (int c = 0; c < 3; ++c) uv[3 + c] = P.Icinv[3 * c] * R.Q[3][6] + P.Icinv[3 * c + 1] * R.Q[4][6] + P.Icinv[3 * c + 2] * R.Q[5][6];
     lds_sync();
     // H_f row i = e_i + E H^ E_i^T: h = H^ E_i^T, then E_j . h = h[k_j] - (d_{l_j} x h_ang)[k_j]
+    // (not needed by the inline solve's rank-6 factor)
     {
+        if constexpr (!(SOLVE && WBC_RANK6)) {
         double h[6];
 #pragma unroll
         for (int ra = 0; ra < 6; ++ra) {
@@ -856,6 +868,7 @@ __device__ bool stance_reduce([[maybe_unused]] const KernelArgs& ka, [[maybe_unu
             cross3(dj, &h[3], cr);
 #pragma unroll
             for (int kj = 0; kj < 3; ++kj) hrow[3 * lj + kj] = ((3 * lj + kj == i) ? 1.0 : 0.0) + h[kj] - cr[kj];
+        }
         }
         // g_f = g_s - E_i Mb^-1 v,  g_s = -E_i (W + [0, 0, g / m, 0, 0, 0])
         double wv[6];
@@ -921,6 +934,218 @@ __device__ bool stance_reduce([[maybe_unused]] const KernelArgs& ka, [[maybe_unu
 }
 
 // ---------------------------------------------------------------------------------------
+// Force-space factor for the inline solve without a 12-step Cholesky (WBC_RANK6).  H_f = I + E Ĥ Eᵀ
+// is the identity plus rank 6 (E = stacked [I, -S(d_l)], 12 x 6), and the dual method needs only
+// some J0 with J0 J0ᵀ = H_f⁻¹ (its iterates do not depend on which).  With EᵀE = L_G L_Gᵀ and
+// Q = E L_G⁻ᵀ (orthonormal columns), H_f = (I - QQᵀ) + Q (I + B) Qᵀ for B = L_Gᵀ Ĥ L_G, so with
+// I + B = L6 L6ᵀ:  J0 = I + Q (L6⁻ᵀ - I) Qᵀ  and  f0 = -J0 J0ᵀ g.  EᵀE = [[4I, -S(D)], [S(D), Σ(|d|² I - d dᵀ)]]
+// (D = Σ d_l) has the block factor L_G = [[2I, 0], [S(D)/2, L22]] with L22 = chol(Σ(|d|² I - d dᵀ) +
+// S(D)²/4), and row i = 3 l + k of Q is [e_k / 2, L22⁻¹ p_k(d_l - D/4)] (p_k(v) = row k of -S(v)).
+// Every lane forms the 6 x 6 quantities (uniform), lane i < 12 its row of J0 and f0_i; the rows go
+// to the J mirror (over Ĥ's LDS, read first) and f0 to ps.xs.  False at a degenerate foot layout.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void pk3(int k, const double* v, double* o) {  // row k of -S(v)
+    o[0] = (k == 0) ? 0.0 : (k == 1) ? -v[2] : v[1];
+    o[1] = (k == 0) ? v[2] : (k == 1) ? 0.0 : -v[0];
+    o[2] = (k == 0) ? -v[1] : (k == 1) ? v[0] : 0.0;
+}
+__device__ bool rank6_factor(const Prob& P, UpdScratch& s, double gsv, int lane) {
+    const int i = lane < 12 ? lane : 11, li = i / 3, ki = i % 3;
+    double Hh[6][6];
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int b = 0; b < 6; ++b) Hh[a][b] = s.sr.S[a][b];
+    double dl[4][3], D[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+    for (int l = 0; l < 4; ++l)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { dl[l][c] = P.d[3 * l + c]; D[c] += dl[l][c]; }
+    double M22[3][3];
+    {
+        const double DD = D[0] * D[0] + D[1] * D[1] + D[2] * D[2];
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int b = 0; b < 3; ++b) M22[a][b] = 0.25 * (D[a] * D[b] - (a == b ? DD : 0.0));
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+            const double dd = dl[l][0] * dl[l][0] + dl[l][1] * dl[l][1] + dl[l][2] * dl[l][2];
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+#pragma unroll
+                for (int b = 0; b < 3; ++b) M22[a][b] += (a == b ? dd : 0.0) - dl[l][a] * dl[l][b];
+        }
+    }
+    // L22 = chol(M22), its reciprocal diagonal
+    const double sc = fmax(M22[0][0], fmax(M22[1][1], M22[2][2]));
+    const double p0 = M22[0][0], r0 = fast_rsq(fmax(p0, 1e-300));
+    const double l00 = p0 * r0, l10 = M22[1][0] * r0, l20 = M22[2][0] * r0;
+    const double p1 = M22[1][1] - l10 * l10, r1 = fast_rsq(fmax(p1, 1e-300));
+    const double l11 = p1 * r1, l21 = (M22[2][1] - l20 * l10) * r1;
+    const double p2 = M22[2][2] - l20 * l20 - l21 * l21, r2 = fast_rsq(fmax(p2, 1e-300));
+    const double l22 = p2 * r2;
+    const bool ok = p0 > 1e-10 * sc && p1 > 1e-10 * sc && p2 > 1e-10 * sc;
+    const double L22[3][3] = {{l00, 0.0, 0.0}, {l10, l11, 0.0}, {l20, l21, l22}};
+    const double SD[3][3] = {{0.0, -D[2], D[1]}, {D[2], 0.0, -D[0]}, {-D[1], D[0], 0.0}};  // S(D)
+    // X = Ĥ L_G, B = L_Gᵀ X (lower triangle), C6 = I + B
+    double X[6][6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            double t = 2.0 * Hh[r][c];
+#pragma unroll
+            for (int m = 0; m < 3; ++m) t = fma(0.5 * Hh[r][3 + m], SD[m][c], t);
+            X[r][c] = t;
+            double u = 0.0;
+#pragma unroll
+            for (int m = c; m < 3; ++m) u = fma(Hh[r][3 + m], L22[m][c], u);
+            X[r][3 + c] = u;
+        }
+    }
+    double C[6][6];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+#pragma unroll
+        for (int c = 0; c <= a; ++c) {
+            double t;
+            if (a < 3) {
+                t = 2.0 * X[a][c];
+#pragma unroll
+                for (int m = 0; m < 3; ++m) t = fma(0.5 * SD[m][a], X[3 + m][c], t);
+            } else {
+                t = 0.0;
+#pragma unroll
+                for (int m = a - 3; m < 3; ++m) t = fma(L22[m][a - 3], X[3 + m][c], t);
+            }
+            C[a][c] = t + (a == c ? 1.0 : 0.0);
+        }
+    }
+    // L6 = chol(C6) in place (lower), id = 1 / diag; Li = L6⁻¹ (lower)
+    double id[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const double ir = fast_rsq(C[k][k]);
+        id[k] = ir;
+        C[k][k] *= ir;
+#pragma unroll
+        for (int a = k + 1; a < 6; ++a) C[a][k] *= ir;
+#pragma unroll
+        for (int a = k + 1; a < 6; ++a)
+#pragma unroll
+            for (int b = k + 1; b <= a; ++b) C[a][b] = fma(-C[a][k], C[b][k], C[a][b]);
+    }
+    double Li[6][6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        Li[j][j] = id[j];
+#pragma unroll
+        for (int a = j + 1; a < 6; ++a) {
+            double t = 0.0;
+#pragma unroll
+            for (int m = j; m < a; ++m) t = fma(C[a][m], Li[m][j], t);
+            Li[a][j] = -t * id[a];
+        }
+    }
+    // lane i: xb_i = L22⁻¹ p_ki(d_li - D/4) (Q_i = [e_ki / 2, xb_i])
+    double ul[4][3];
+#pragma unroll
+    for (int l = 0; l < 4; ++l)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) ul[l][c] = dl[l][c] - 0.25 * D[c];
+    auto l22solve = [&](const double* v, double* o) {  // L22 o = v
+        o[0] = v[0] * r0;
+        o[1] = (v[1] - l10 * o[0]) * r1;
+        o[2] = (v[2] - l20 * o[0] - l21 * o[1]) * r2;
+    };
+    double xb[3];
+    {
+        const double u3[3] = {sel4d(li, ul[0][0], ul[1][0], ul[2][0], ul[3][0]), sel4d(li, ul[0][1], ul[1][1], ul[2][1], ul[3][1]),
+                              sel4d(li, ul[0][2], ul[1][2], ul[2][2], ul[3][2])};
+        double pv[3];
+        pk3(ki, u3, pv);
+        l22solve(pv, xb);
+    }
+    const double qt[3] = {ki == 0 ? 0.5 : 0.0, ki == 1 ? 0.5 : 0.0, ki == 2 ? 0.5 : 0.0};
+    // a_i = Q_i T, T = Liᵀ - I: a[c] = sum_{r <= c} Q_i[r] Li[c][r] - Q_i[c]
+    const double Qi[6] = {qt[0], qt[1], qt[2], xb[0], xb[1], xb[2]};
+    double ai[6];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+        double t = -Qi[c];
+#pragma unroll
+        for (int r = 0; r <= c; ++r) t = fma(Qi[r], Li[c][r], t);
+        ai[c] = t;
+    }
+    // b_i = L22⁻ᵀ a_i[3..5]; J0[i][j] = delta_ij + a_i[kj] / 2 + b_i . p_kj(u_lj)
+    double bi[3];
+    bi[2] = ai[5] * r2;
+    bi[1] = (ai[4] - l21 * bi[2]) * r1;
+    bi[0] = (ai[3] - l10 * bi[1] - l20 * bi[2]) * r0;
+    double J0[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+        double pv[3];
+        pk3(j % 3, ul[j / 3], pv);
+        J0[j] = ((i == j) ? 1.0 : 0.0) + 0.5 * ai[j % 3] + (bi[0] * pv[0] + bi[1] * pv[1] + bi[2] * pv[2]);
+    }
+    // f0 = -J0 J0ᵀ g: Eᵀ v = [sum_l v_l, sum_l d_l x v_l]; q6 = L_G⁻¹ Eᵀ v
+    auto q6_of = [&](double vv, double* q6) {
+        double top[3] = {0.0, 0.0, 0.0}, bot[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+            const double v3[3] = {seg_bcast<16>(vv, 3 * l), seg_bcast<16>(vv, 3 * l + 1), seg_bcast<16>(vv, 3 * l + 2)};
+            double cr[3];
+            cross3(dl[l], v3, cr);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) { top[c] += v3[c]; bot[c] += cr[c]; }
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) q6[c] = 0.5 * top[c];
+        double dq[3], rhs[3];
+        cross3(D, q6, dq);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) rhs[c] = bot[c] - 0.5 * dq[c];
+        l22solve(rhs, &q6[3]);
+    };
+    double q6[6];
+    q6_of(gsv, q6);
+    double w[6];  // w = Tᵀ q6 = Li q6 - q6
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+        double t = -q6[c];
+#pragma unroll
+        for (int r = 0; r <= c; ++r) t = fma(Li[c][r], q6[r], t);
+        w[c] = t;
+    }
+    double y = gsv;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) y = fma(Qi[c], w[c], y);
+    q6_of(y, q6);
+    double v[6];  // v = T q6 = Liᵀ q6 - q6
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+        double t = -q6[c];
+#pragma unroll
+        for (int r = c; r < 6; ++r) t = fma(Li[r][c], q6[r], t);
+        v[c] = t;
+    }
+    double f0 = y;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) f0 = fma(Qi[c], v[c], f0);
+    lds_sync();  // every lane has read Ĥ before the mirror overwrites it
+    if (lane < 12) {
+        double* Jl = &s.ps.L[0][0];
+#pragma unroll
+        for (int j = 0; j < 12; j += 2) *reinterpret_cast<double2*>(&Jl[i * 12 + j]) = make_double2(J0[j], J0[j + 1]);
+        s.ps.xs[i] = -f0;
+    }
+    lds_sync();
+    return !seg_any<16>(!ok);
+}
+
+// ---------------------------------------------------------------------------------------
 // inline stance solve: the 12-variable force-space QP of a four-contact robot whose equalities
 // stance_reduce eliminated, solved by its own 16-lane segment of the update wave (four robots per
 // wave) right after factor12, so that nothing of it passes through HBM.  The Goldfarb-Idnani
@@ -962,6 +1187,8 @@ __device__ __forceinline__ int seg_shfl_i(int v, int j) {
 }
 __device__ __forceinline__ double sel3d(int j, double a, double b, double c) { return j == 0 ? a : (j == 1 ? b : c); }
 
+// ROWS: the J mirror already holds J0 by rows (rank6_factor); otherwise M = L^-1 (factor12)
+template <bool ROWS>
 __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, const Prob& P, UpdScratch& s) {
     constexpr int N = 12;
     const wbc_params& pr = *a.params;
@@ -1009,7 +1236,7 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
     // J = L^-T (row l of J = column l of M in lane l < 12), the primal x = f0 (x_l in lane l)
     double Jr[N];
 #pragma unroll
-    for (int j = 0; j < N; ++j) Jr[j] = (l < N) ? Jl[j * 12 + i] : 0.0;
+    for (int j = 0; j < N; ++j) Jr[j] = (l < N) ? (ROWS ? Jl[i * 12 + j] : Jl[j * 12 + i]) : 0.0;
     double x = (l < N) ? s.ps.xs[i] : 0.0;
     lds_sync();  // every lane has read M before the mirror overwrites it
     auto mirror = [&]() {
@@ -1019,7 +1246,7 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
         }
         lds_sync();
     };
-    mirror();
+    if (!ROWS) mirror();
     UST(a, rb, 15);  // normals, slacks, J
 
     double rinv[N];  // row l of R^-1 (l < 12)
@@ -1889,13 +2116,23 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
         }
         const bool fact = stance || !a.modes;
         if (fact) {
+            if constexpr (SOLVE && SUB == 16 && WBC_RANK6) {
+                if (stance) {
+                    if (rank6_factor(P, s, gsv, lane)) {
+                        UST(a, rb, 11);
+                        solve_stance16<true>(a, rb, lane, wr, P, s);
+                        return true;
+                    }
+                    stance = false;  // degenerate foot layout: the general path
+                }
+            }
             if (!stance) slot_hessian_row(P, kap, pr, lane, hrow, gsv);
-            const bool ok = factor12<SUB>(hrow, gsv, lane, s.ps.L, s.ps.ild, s.ps.xs);
+            const bool ok = factor12<SUB>(hrow, gsv, lane, s.ps.L, s.ps.ild, s.ps.xs, &a, rb);
             const double (&Mi)[12][12] = *reinterpret_cast<const double(*)[12][12]>(&s.ps.L[0][0]);
-            if constexpr (SOLVE && SUB == 16) {
+            if constexpr (SOLVE && SUB == 16 && !WBC_RANK6) {
                 if (stance && ok) {
                     UST(a, rb, 11);
-                    solve_stance16(a, rb, lane, wr, P, s);
+                    solve_stance16<false>(a, rb, lane, wr, P, s);
                     return true;
                 }
             }

@@ -36,6 +36,11 @@ if ok2.any() and (s3[ok2] > 0).all():
     res["stance: Y, q0"] = float(np.median(s3[ok2, 0] - st[ok2, 0]))
     res["stance: Q = Y^T Y"] = float(np.median(s3[ok2, 1] - s3[ok2, 0]))
     res["stance: H^, H_f row, g_f"] = float(np.median(st[ok2, 1] - s3[ok2, 1]))
+f2 = e.debug()[0::4, 31:33]  # stamps 23, 24 inside factor12
+if ok2.any() and (f2[ok2] > 0).all():
+    res["factor: Cholesky"] = float(np.median(f2[ok2, 0] - st[ok2, 2]))
+    res["factor: M = L^-1"] = float(np.median(f2[ok2, 1] - f2[ok2, 0]))
+    res["factor: f0"] = float(np.median(u[ok2, 11] - f2[ok2, 1]))
 if ok2.any():
     res["stance: Gauss-Jordan"] = float(np.median(st[ok2, 0] - u[ok2, 10]))
     res["stance: H_f row"] = float(np.median(st[ok2, 1] - st[ok2, 0]))
