@@ -116,6 +116,24 @@ def test_stance_stress_inline_matches_oracle(max_torque, seed):
         assert close(inl["x"][b], o["x"][b], 1e-8), b
 
 
+@pytest.mark.parametrize("max_wsr", [1, 2, 3])
+def test_inline_max_iter_matches_oracle(max_wsr):
+    """The nWSR cap (cpp:517) inside the inline solve: WBC_QP_MAX_ITER exactly where the C oracle
+    hits it on all-stance states, iterations capped at max_wsr, zeros published."""
+    inp = workloads.stance_cold(256, seed=70 + max_wsr)  # 0-10 working-set changes per QP
+    p = default_params()
+    p.max_wsr = max_wsr
+    out = run(inp, params=p)
+    o = R.run_batch(inp, max_wsr=max_wsr)
+    assert np.array_equal(out["status"], o["status"])
+    capped = o["status"] == 1  # WBC_QP_MAX_ITER
+    assert capped.sum() > 0 and (o["status"] == 0).sum() > 0
+    assert np.all(out["iters"][capped] == max_wsr)
+    assert np.all(out["tau"][capped] == 0.0) and np.all(out["x"][capped] == 0.0)
+    for b in np.nonzero(o["status"] == 0)[0]:
+        assert close(out["tau"][b], o["tau"][b], 1e-7), b
+
+
 def test_straight_knee_falls_back_and_matches_oracle():
     B = 96
     inp = workloads.stance_cold(B, seed=12)
