@@ -1159,9 +1159,6 @@ __device__ bool rank6_factor(const Prob& P, UpdScratch& s, double gsv, int lane)
 // updated with every step (no recovery pass).  Cold start only: the engine uses it for stateless
 // all-stance steps.
 // ---------------------------------------------------------------------------------------
-#ifndef WBC_NPLUS_DIRECT
-#define WBC_NPLUS_DIRECT 0  // 1 measured slower: B = 4096 stance 88.0 -> 80.3 M solves/s (profiles/r02/s/var_np.log)
-#endif
 // min over each 16-lane DPP row of a value tagged with a 6-bit index (as wave_argmin_lane: ties to
 // the lowest index); returns the index, uniform over the row
 __device__ __forceinline__ double tag6(double v, int idx) {
@@ -1256,45 +1253,27 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
     double u = 0.0, up = 0.0;
     bool done = (status != WBC_QP_OK);
     const int max_wsr = pr.max_wsr;
+    // most violated row, by slack / |reference row| (ties to the lowest row); none: optimal.  Run
+    // before the loop and then right after each add, where it overlaps the Householder update of J
+    auto select = [&]() {
+        const double w0 = (!(ab & 1) && sp0 < -tol0) ? sp0 * in0 : 1e300;
+        const double w1 = (!(ab & 2) && sp1 < -tol1) ? sp1 * in1 : 1e300;
+        const double w2 = (v2 && !(ab & 4) && sp2 < -tol2) ? sp2 * in2 : 1e300;
+        const double m = seg16_min(fmin(tag6(w0, l), fmin(tag6(w1, 16 + l), tag6(w2, 32 + l))));
+        if (!(m < 1e299)) done = true;
+        pstar = untag6(m);
+        up = 0.0;
+    };
+    if (!done) select();
 
     while (__any(!done)) {
-        // column i of J from the mirror, issued before the selection so that its LDS latency is
-        // off the step's dependency chain
+        // column i of J from the mirror, issued first so that its LDS latency is off the chain
         double jc[N];
 #pragma unroll
         for (int k = 0; k < N; ++k) jc[k] = Jl[k * 12 + i];
-        if (!done) {
-            if (pstar < 0) {  // most violated row, by slack / |reference row|
-                const double w0 = (!(ab & 1) && sp0 < -tol0) ? sp0 * in0 : 1e300;
-                const double w1 = (!(ab & 2) && sp1 < -tol1) ? sp1 * in1 : 1e300;
-                const double w2 = (v2 && !(ab & 4) && sp2 < -tol2) ? sp2 * in2 : 1e300;
-                const double m = seg16_min(fmin(tag6(w0, l), fmin(tag6(w1, 16 + l), tag6(w2, 32 + l))));
-                if (!(m < 1e299)) done = true;  // optimal
-                pstar = untag6(m);
-                up = 0.0;
-            }
-            if (!done && ++iters > max_wsr) { status = WBC_QP_MAX_ITER; iters = max_wsr; done = true; }
-        }
+        if (!done && ++iters > max_wsr) { status = WBC_QP_MAX_ITER; iters = max_wsr; done = true; }
         if (!done) {
             const int pos = q, ol = pstar & 15, js = pstar >> 4;
-#if WBC_NPLUS_DIRECT
-            // the chosen row's normal n+ (friction pattern, or +- a row of Nt), formed by every
-            // lane; its slack from its lane by a DPP sum (no LDS round trip on the chain)
-            double np[N];
-            {
-                const bool isf = pstar < 16;
-                const int pl = pstar >> 2, rp = pstar & 3, qt = isf ? 0 : pstar - 16;
-                const double sgn = (qt & 1) ? 1.0 : -1.0;
-                const double fr0 = (rp == 0) ? -1.0 : (rp == 1 ? 1.0 : 0.0), fr1 = (rp == 2) ? -1.0 : (rp == 3 ? 1.0 : 0.0);
-                const double* nt = V.Nt + (qt >> 1) * 12;
-#pragma unroll
-                for (int m = 0; m < N; ++m) {
-                    const double fv = (m % 3 == 0) ? fr0 : (m % 3 == 1) ? fr1 : pr.friction;
-                    np[m] = isf ? ((m / 3 == pl) ? fv : 0.0) : sgn * nt[m];
-                }
-            }
-            const double sps = seg_sum<16>((l == ol) ? sel3d(js, sp0, sp1, sp2) : 0.0);
-#else
             if (l == ol) {  // the chosen row's normal and slack, from its lane
 #pragma unroll
                 for (int k = 0; k < N; ++k) V.col[k] = sel3d(js, n0[k], n1[k], n2[k]);
@@ -1305,7 +1284,6 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
 #pragma unroll
             for (int k = 0; k < N; ++k) np[k] = V.col[k];
             const double sps = V.col[12];
-#endif
             // d = J^T n+ (lane j: column j of the mirror), then to every lane
             double dj;
             {
@@ -1375,6 +1353,10 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
                 if (l < q) u -= t * rk;
                 up += t;
                 if (full) {
+                    if (l == q) { u = up; act = pstar; }
+                    if (l == ol) ab |= 1 << js;
+                    ++q;
+                    select();  // the next row: slacks and active flags are final, J is not needed
                     // Householder add: J <- J H on columns pos.. (row l: v . J_l = z_l - alpha J_l[pos]);
                     // R^-1 gains the column [-r / alpha; 1 / alpha]
                     const double rs = fast_rsq(zn);
@@ -1389,10 +1371,6 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
                     const bool wcol = l <= pos;
 #pragma unroll
                     for (int k = 0; k < N; ++k) rinv[k] = (wcol && k == pos) ? nv : rinv[k];
-                    if (l == q) { u = up; act = pstar; }
-                    if (l == ol) ab |= 1 << js;
-                    ++q;
-                    pstar = -1;
                 } else {
                     // drop slot l1: shift the active lists, then Givens deletion (givens_drop) with the
                     // rotation of step k from the R column of the row now in slot k: (J^T n)[k, k+1]
