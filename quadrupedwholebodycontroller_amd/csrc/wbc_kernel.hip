@@ -3399,6 +3399,47 @@ WBC_KERNEL_ATTR void wbc_step_kernel(KernelArgs a) {
 // The update kernel, and (SOLVE) its form that also solves the four-contact stance QPs whose
 // elimination succeeded (wbc_update_solve_kernel: stateless all-stance steps; the problem of such
 // a robot never goes to HBM, only its outputs do).
+// Copy N elements global -> LDS with every load issued before the first store: one memory round
+// trip.  The plain strided loop (`for (k = lane; k < N; k += 64) dst[k] = src[k]`) has a
+// lane-dependent trip count, so it is not unrolled and each iteration waits for its own load
+// (s_waitcnt vmcnt(0) before the ds_write): N / 64 serialized round trips.
+template <int N>
+__device__ __forceinline__ void stage_to_lds(double* dst, const double* src, int t) {
+    constexpr int IT = (N + 63) / 64;
+    double v[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int k = t + 64 * it;
+        v[it] = src[k < N ? k : N - 1];
+    }
+    __builtin_amdgcn_sched_barrier(0);  // the scheduler may not sink a load below the first store
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int k = t + 64 * it;
+        dst[k < N ? k : N - 1] = v[it];  // branch-free: lanes past the end rewrite the last element, same value
+    }
+}
+// the same for 16-byte elements (kept as two scalar arrays: a local array of double2 is not
+// promoted to registers here and goes through scratch)
+template <int N>
+__device__ __forceinline__ void stage_to_lds(double2* dst, const double2* src, int t) {
+    constexpr int IT = (N + 63) / 64;
+    double vx[IT], vy[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int k = t + 64 * it;
+        const double2 w = src[k < N ? k : N - 1];
+        vx[it] = w.x;
+        vy[it] = w.y;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int k = t + 64 * it;
+        dst[k < N ? k : N - 1] = make_double2(vx[it], vy[it]);
+    }
+}
+
 template <bool SOLVE>
 __device__ __forceinline__ void update_kernel_body(const KernelArgs& a) {
     __shared__ UpdLds L;
@@ -3412,11 +3453,8 @@ __device__ __forceinline__ void update_kernel_body(const KernelArgs& a) {
     }
     const bool wr = rb < a.batch;  // a padding segment recomputes the last robot, writes nothing
     if (!wr) rb = a.batch - 1;
-    {
-        const double* gm = reinterpret_cast<const double*>(a.model);
-        double* lm = reinterpret_cast<double*>(&L.model);
-        for (int k = (int)threadIdx.x; k < (int)(sizeof(wbc_model) / 8); k += 64) lm[k] = gm[k];
-    }
+    stage_to_lds<(int)(sizeof(wbc_model) / 8)>(reinterpret_cast<double*>(&L.model),
+                                                reinterpret_cast<const double*>(a.model), (int)threadIdx.x);
     lds_sync();
     // work row: [Prob | Presolve]; the Presolve record is stored by update_phase itself
     Presolve* pre = reinterpret_cast<Presolve*>(a.work + (size_t)rb * WORK_LEN + PROB_LEN);
@@ -3494,9 +3532,8 @@ __device__ void solve_general_qp(const KernelArgs& a, int rb, SolveLds& L) {
     pf.v0 = prow[lane_id()];
     pf.v1 = prow[64 + lane_id()];
     const int kap_qp = qp_mask(a, rb, row);
-    double2* dst = reinterpret_cast<double2*>(&L.prob);
-    const double2* src = reinterpret_cast<const double2*>(a.work + (size_t)row * WORK_LEN);
-    for (int k = lane_id(); k < PROB_LEN / 2; k += 64) dst[k] = src[k];
+    stage_to_lds<PROB_LEN / 2>(reinterpret_cast<double2*>(&L.prob),
+                               reinterpret_cast<const double2*>(a.work + (size_t)row * WORK_LEN), lane_id());
     // the stance kernel's QP: checked after the problem copy is issued, so that a general QP's
     // loads all go out together (one HBM round trip)
     if (WBC_STANCE_KERNEL && WBC_STANCE_ELIM && a.elim && kap_qp == 15 && bcast(pf.v1, PRE_STANCE - 64) != 0.0) return;
