@@ -43,6 +43,7 @@ struct wbc_engine {
     hipStream_t stream = nullptr;
     wbc_model* d_model = nullptr;
     wbc_params* d_params = nullptr;
+    wbc_params params{};  // host copy, passed by value in the kernel arguments (KernelArgs::pv)
     // owned inputs: one device block [pose | nu | qj | ref | contacts | switching] (so a host cycle
     // is one H2D copy), and the outputs one block [tau | grf | status | iters | x]
     void* d_inblk = nullptr;
@@ -117,6 +118,7 @@ wbc::KernelArgs make_args(wbc_engine* h, uint32_t flags) {
     wbc::KernelArgs a;
     a.model = h->d_model;
     a.params = h->d_params;
+    a.pv = h->params;
     a.base_pose = h->in_pose;
     a.nu = h->in_nu;
     a.qj = h->in_qj;
@@ -223,6 +225,7 @@ int32_t wbc_create(const wbc_model* model, const wbc_params* params, int32_t bat
         delete h;
         return fail(WBC_ERR_ARG, "wbc_create: invalid params");
     }
+    h->params = p;
     const size_t B = (size_t)batch;
 #define ALLOC(ptr, n)                                             \
     if (dalloc(&h->ptr, (n)) != hipSuccess) {                     \

@@ -1188,7 +1188,7 @@ __device__ __forceinline__ double sel3d(int j, double a, double b, double c) { r
 template <bool ROWS>
 __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, const Prob& P, UpdScratch& s) {
     constexpr int N = 12;
-    const wbc_params& pr = *a.params;
+    const wbc_params& pr = a.pv;
     const St16 V(s);
     double* Jl = &s.ps.L[0][0];  // M = L^-1 (row-major 12 x 12) on entry, then the LDS mirror of J
     const int i = l < N ? l : 0;
@@ -1477,7 +1477,7 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
 template <int SUB, bool SOLVE = false>
 __device__ bool update_phase(const KernelArgs& a, int rb, int lane, bool wr, UpdScratch& s, Prob& P, Presolve* pre,
                              const wbc_model& md) {
-    const wbc_params& pr = *a.params;
+    const wbc_params& pr = a.pv;
     const int kap = a.contacts[rb];
     const bool switching = a.switching[rb] != 0;
     const bool stateful = a.stateful != 0;
@@ -1779,14 +1779,37 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
     double y[6] = {0, 0, 0, 0, 0, 0};
     bool hvalid = false;
     int kap_old = 15;
+    // The old history this lane reads, loaded in one batch (addresses clamped, so every lane loads
+    // unconditionally).  Read where they are used, the loads sit in lane-dependent branches and
+    // after history stores the compiler cannot order them against, so it issued and waited for
+    // them group by group: about ten serialized memory round trips per stateful update.
+    constexpr int NT = (18 + SUB - 1) / SUB;  // Tdot_inv columns per lane
+    double hTd[18], hMa[NT][6], hR[3], hDo[3], hJo[12], hE = 0.0;
     if (stateful) {
-        hvalid = H[H_VALID] != 0.0;
-        kap_old = (int)H[H_KOLD];
+        const int l6 = lane < 6 ? lane : 5, l12 = lane < 12 ? lane : 11;
+        const double hv = H[H_VALID], hk = H[H_KOLD];
+#pragma unroll
+        for (int cc = 0; cc < 18; ++cc) hTd[cc] = H[H_TDINV + l6 * 18 + cc];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) hR[i] = H[H_ROLD + i];
+#pragma unroll
+        for (int it = 0; it < NT; ++it) {
+            const int jj = lane + it * SUB - 6, j = jj < 0 ? 0 : (jj > 11 ? 11 : jj);
+#pragma unroll
+            for (int rr = 0; rr < 6; ++rr) hMa[it][rr] = H[H_MAOLD + rr * 12 + j];
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) hDo[k] = H[H_DOLD + 3 * (l12 / 3) + k];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) hJo[j] = H[H_JBJOLD + l12 * 12 + j];
+        hE = H[H_EINT + l6];
+        hvalid = hv != 0.0;
+        kap_old = (int)hk;
         if (hvalid) {
             double yl = 0.0;
             if (lane < 6) {
 #pragma unroll
-                for (int cc = 0; cc < 18; ++cc) yl += H[H_TDINV + lane * 18 + cc] * s.in[7 + cc];
+                for (int cc = 0; cc < 18; ++cc) yl += hTd[cc] * s.in[7 + cc];
             }
             if constexpr (SUB == 64) {
 #pragma unroll
@@ -1875,7 +1898,6 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
     }
     UST(a, rb, 8);
     // T_top = [Ad^-1(r), Mbar_b^-1 A_j]; Tdot_inv for the next cycle (cpp:291-293)
-    constexpr int NT = (18 + SUB - 1) / SUB;  // Tdot_inv columns per lane
     double tcol[NT][6];
 #pragma unroll
     for (int it = 0; it < NT; ++it)
@@ -1885,7 +1907,7 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
         double dr[3] = {0, 0, 0};
         if (!switching) {
 #pragma unroll
-            for (int i = 0; i < 3; ++i) dr[i] = (r[i] - H[H_ROLD + i]) / dt;
+            for (int i = 0; i < 3; ++i) dr[i] = (r[i] - hR[i]) / dt;
         }
 #pragma unroll
         for (int it = 0; it < NT; ++it) {
@@ -1899,8 +1921,8 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
             double Tj[6];
 #pragma unroll
             for (int rr = 0; rr < 3; ++rr) {
-                Tj[rr] = switching ? 0.0 : (s.A[j][rr] * inv_m - H[H_MAOLD + rr * 12 + j]) / dt;
-                Tj[3 + rr] = switching ? 0.0 : (s.KA[j][rr] - H[H_MAOLD + (3 + rr) * 12 + j]) / dt;
+                Tj[rr] = switching ? 0.0 : (s.A[j][rr] * inv_m - hMa[it][rr]) / dt;
+                Tj[3 + rr] = switching ? 0.0 : (s.KA[j][rr] - hMa[it][3 + rr]) / dt;
             }
             double t1[3], t2[3];
             cross3(dr, s.KA[j], t1);
@@ -1945,12 +1967,12 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
         for (int j = 0; j < 12; ++j) cur += P.Jbj[i * 12 + j] * qd[j];
         double old = 0.0;
         if (stateful && hvalid) {
-            const double dol[3] = {H[H_DOLD + 3 * l], H[H_DOLD + 3 * l + 1], H[H_DOLD + 3 * l + 2]};
+            const double dol[3] = {hDo[0], hDo[1], hDo[2]};
             double wxo[3];
             cross3(w3, dol, wxo);
             old = s.cen[CEN_VC + rr] + sel3(wxo, rr);
 #pragma unroll
-            for (int j = 0; j < 12; ++j) old += H[H_JBJOLD + i * 12 + j] * qd[j];
+            for (int j = 0; j < 12; ++j) old += hJo[j] * qd[j];
         }
         // mode hypotheses (a.modes > 0, stateless): both bounds unmasked, the R1 bound as for a stance
         // leg and the swing bound as for a swing leg; the solve kernel masks them per hypothesis
@@ -1971,7 +1993,7 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
     if (lane < 6) {
         const int k = lane;
         const double kp = (k == 2) ? pr.kp_z : pr.kp;
-        const double eint = (stateful && hvalid) ? H[H_EINT + k] : 0.0;
+        const double eint = (stateful && hvalid) ? hE : 0.0;
         double mba;
         if (k < 3) mba = m * ref[12 + k];
         else mba = P.Ic[3 * (k - 3)] * ref[15] + P.Ic[3 * (k - 3) + 1] * ref[16] + P.Ic[3 * (k - 3) + 2] * ref[17];
@@ -2439,7 +2461,7 @@ static_assert(offsetof(Presolve, presolved) == PRE_FLAG * sizeof(double), "PRE_F
 static_assert(offsetof(Presolve, xs) == 78 * sizeof(double), "Presolve packing");
 
 __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, const PreRegs* pf, QpScratch& s) {
-    const wbc_params& pr = *a.params;
+    const wbc_params& pr = a.pv;
     const int lane = lane_id();
     const int kap = (int)P.kappa;
     const QpMap mp = make_map(kap);
@@ -3013,7 +3035,7 @@ __device__ void solve_stance(const KernelArgs& a, int rb, const Prob* Pg, const 
                              StanceScratch& s) {
     const Prob& P = *Pg;  // the assembled problem in HBM / L2: only flags, bbar_j and the x-output fields are read
     constexpr int N = StanceScratch::N, MC = StanceScratch::MC, NEQ = 12;
-    const wbc_params& pr = *a.params;
+    const wbc_params& pr = a.pv;
     const int lane = lane_id();
     STAMP(a, rb, 0);
     int status = (P.flags != 0.0) ? WBC_QP_NUMERIC : WBC_QP_OK;
@@ -3315,8 +3337,9 @@ __device__ void solve_stance(const KernelArgs& a, int rb, const Prob* Pg, const 
         if (lane < 42) {
             double xv;
             if (lane < 6) {
-                xv = sel3(bf, lane < 3 ? lane : 0);
-                xv = (lane < 3) ? xv - (lane == 2 ? pr.gravity : 0.0) : sel3(&bf[3], lane < 3 ? 0 : lane - 3);
+                // selects on scalars (sel3 on the local array was lowered to a scratch load)
+                xv = sel3d(lane < 3 ? lane : 0, bf[0], bf[1], bf[2]);
+                xv = (lane < 3) ? xv - (lane == 2 ? pr.gravity : 0.0) : sel3d(lane < 3 ? 0 : lane - 3, bf[3], bf[4], bf[5]);
             } else if (lane < 18) {
                 const int j = lane - 6;
                 const double* yr = rec->Y + j * 6;

@@ -102,6 +102,10 @@ struct KernelArgs {
     int32_t elim;
     int32_t parity;
     int32_t* fb;
+    // the parameters by value: read from the kernel-argument segment (scalar loads of memory the
+    // compiler knows is constant), not through `params`, whose global loads it must repeat after
+    // every global store and wait for in turn
+    wbc_params pv;
 };
 
 
