@@ -1184,6 +1184,10 @@ __device__ __forceinline__ int seg_shfl_i(int v, int j) {
 }
 __device__ __forceinline__ double sel3d(int j, double a, double b, double c) { return j == 0 ? a : (j == 1 ? b : c); }
 
+// 1: d[pos] and J[l][pos] as 12-term sums against a row mask (the form before round 2's A/B)
+#ifndef WBC_INLINE_MASKSUM
+#define WBC_INLINE_MASKSUM 0
+#endif
 // ROWS: the J mirror already holds J0 by rows (rank6_factor); otherwise M = L^-1 (factor12)
 template <bool ROWS>
 __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, const Prob& P, UpdScratch& s) {
@@ -1296,20 +1300,25 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
             double d[N], d2[N];
 #pragma unroll
             for (int k = 0; k < N; ++k) d[k] = seg_bcast<16>(dj, k);
-            double rk, zn, dq;
+            // d[pos] and J[l][pos] (needed only by the Householder add, so their LDS latency is
+            // off the chain): from lane pos of the segment and from the J mirror, instead of
+            // 12-term sums against a 0 / 1 row mask (pos varies by segment)
+            const double dq = WBC_INLINE_MASKSUM ? 0.0 : seg_shfl(dj, pos);  // lane 12.. holds 0
+            const double jqm = (WBC_INLINE_MASKSUM || l >= N || pos >= N) ? 0.0 : Jl[i * 12 + (pos < N ? pos : 0)];
+            double rk, zn, dqs;
             {
                 double acc[4] = {0.0, 0.0, 0.0, 0.0}, zz[4] = {0, 0, 0, 0}, ee[4] = {0, 0, 0, 0};
 #pragma unroll
                 for (int j = 0; j < N; ++j) {
-                    const double mk = (j >= pos) ? 1.0 : 0.0, ok = (j == pos) ? 1.0 : 0.0;
+                    const double mk = (j >= pos) ? 1.0 : 0.0;
                     acc[j & 3] += rinv[j] * d[j];
                     d2[j] = d[j] * mk;
                     zz[j & 3] += d[j] * d2[j];
-                    ee[j & 3] += d[j] * ok;
+                    if (WBC_INLINE_MASKSUM) ee[j & 3] += d[j] * ((j == pos) ? 1.0 : 0.0);
                 }
                 rk = (l < N) ? (acc[0] + acc[1]) + (acc[2] + acc[3]) : 0.0;
                 zn = (zz[0] + zz[1]) + (zz[2] + zz[3]);
-                dq = (ee[0] + ee[1]) + (ee[2] + ee[3]);
+                dqs = WBC_INLINE_MASKSUM ? (ee[0] + ee[1]) + (ee[2] + ee[3]) : dq;
             }
             // primal direction z = J2 d2 (lane k: z_k), then to every lane; slack rates n . z
             double zk, jq;
@@ -1318,10 +1327,10 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
 #pragma unroll
                 for (int j = 0; j < N; ++j) {
                     acc[j & 3] += Jr[j] * d2[j];
-                    e4[j & 3] += Jr[j] * ((j == pos) ? 1.0 : 0.0);
+                    if (WBC_INLINE_MASKSUM) e4[j & 3] += Jr[j] * ((j == pos) ? 1.0 : 0.0);
                 }
                 zk = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-                jq = (e4[0] + e4[1]) + (e4[2] + e4[3]);
+                jq = WBC_INLINE_MASKSUM ? (e4[0] + e4[1]) + (e4[2] + e4[3]) : jqm;
             }
             double cz0, cz1, cz2;
             {
@@ -1361,16 +1370,24 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
                     // R^-1 gains the column [-r / alpha; 1 / alpha]
                     const double rs = fast_rsq(zn);
                     const double nrm2 = zn * rs;
-                    const double alpha = (dq >= 0.0) ? -nrm2 : nrm2;
-                    const double ia = (dq >= 0.0) ? -rs : rs;
-                    const double beta = fast_rcp(zn + nrm2 * fabs(dq));
+                    const double alpha = (dqs >= 0.0) ? -nrm2 : nrm2;
+                    const double ia = (dqs >= 0.0) ? -rs : rs;
+                    const double beta = fast_rcp(zn + nrm2 * fabs(dqs));
                     const double vw = (zk - alpha * jq) * beta, vwa = vw * alpha;
 #pragma unroll
                     for (int k = 0; k < N; ++k) Jr[k] = fma(vwa, (k == pos) ? 1.0 : 0.0, fma(-vw, d2[k], Jr[k]));
                     const double nv = (l == pos) ? ia : -rk * ia;
                     const bool wcol = l <= pos;
+                    if (WBC_INLINE_MASKSUM) {
 #pragma unroll
-                    for (int k = 0; k < N; ++k) rinv[k] = (wcol && k == pos) ? nv : rinv[k];
+                        for (int k = 0; k < N; ++k) rinv[k] = (wcol && k == pos) ? nv : rinv[k];
+                    } else {
+                        // column pos of R^-1 is 0 before the add and nv is finite here (zn > 1e-14),
+                        // so adding nv under the 0 / 1 mask is exact
+                        const double nvw = wcol ? nv : 0.0;
+#pragma unroll
+                        for (int k = 0; k < N; ++k) rinv[k] = fma((k == pos) ? 1.0 : 0.0, nvw, rinv[k]);
+                    }
                 } else {
                     // drop slot l1: shift the active lists, then Givens deletion (givens_drop) with the
                     // rotation of step k from the R column of the row now in slot k: (J^T n)[k, k+1]
