@@ -175,11 +175,22 @@ __device__ __forceinline__ double vbcast(double v, int lane) {
 // DPP moves whose pattern reads a valid lane for every lane (quad_perm, row_ror, row_mirror,
 // row_newbcast): v_mov_b32_dpp without an "old" operand (update_dpp(0, ...) makes the compiler
 // zero the destination first, one extra move per 32-bit half)
+// row_newbcast (0x150 + lane) is the one pattern gfx950 allows on 64-bit DPP: one v_mov_b64_dpp
+// instead of two v_mov_b32_dpp (WBC_DPP64=0 keeps the 32-bit pair, the earlier form)
+#ifndef WBC_DPP64
+#define WBC_DPP64 1
+#endif
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double v) {
-    int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
-    int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
-    return __hiloint2double(hi, lo);
+    if constexpr (WBC_DPP64 && CTRL >= 0x150 && CTRL <= 0x15F) {
+        const long long b = __builtin_bit_cast(long long, v);
+        const long long r = __builtin_amdgcn_mov_dpp(b, CTRL, 0xF, 0xF, false);
+        return __builtin_bit_cast(double, r);
+    } else {
+        int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+        int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+        return __hiloint2double(hi, lo);
+    }
 }
 // Lane j (a constant once the caller's loops are unrolled) of the robot's lane segment, to every
 // lane of the segment: v_readlane for one robot per wave, DPP row_newbcast for 16-lane segments
