@@ -3629,6 +3629,13 @@ void wbc_solve_stance_kernel(KernelArgs a) {
                  reinterpret_cast<const Presolve*>(prow), S);
 }
 
+#ifndef WBC_AB_FB_EMPTY
+#define WBC_AB_FB_EMPTY 0
+#endif
+__global__ void wbc_empty_kernel(int32_t* fb, int parity) {
+    if (fb[parity] < 0) fb[2] = 0;  // never true; keeps the load
+}
+
 __global__ void wbc_reset_kernel(double* hist, const uint8_t* mask, int batch) {
     const int rb = xcd_robot();
     if (rb >= batch) return;
@@ -3670,7 +3677,11 @@ extern "C" hipError_t wbc_launch_update_solve(const wbc::KernelArgs* a, hipStrea
     if (!WBC_STANCE_ELIM || !a->elim || a->stateful || a->modes) return hipErrorInvalidValue;
     hipLaunchKernelGGL(wbc::wbc_update_solve_kernel, dim3((a->batch + wbc::UPD_RPW - 1) / wbc::UPD_RPW), dim3(64), 0,
                        st, *a);
+#if WBC_AB_FB_EMPTY  // A/B timing builds only: an empty kernel in the fallback's place (not a correct solve)
+    hipLaunchKernelGGL(wbc::wbc_empty_kernel, dim3(16), dim3(64), 0, st, a->fb, a->parity);
+#elif !WBC_AB_NO_FALLBACK
     hipLaunchKernelGGL(wbc::wbc_solve_fallback_kernel, dim3(16), dim3(64), 0, st, *a);
+#endif
     return hipGetLastError();
 }
 extern "C" hipError_t wbc_launch_reset(double* hist, const uint8_t* mask, int batch, hipStream_t st) {
