@@ -1199,6 +1199,11 @@ __device__ __forceinline__ double sel3d(int j, double a, double b, double c) { r
 #ifndef WBC_INLINE_MASKSUM
 #define WBC_INLINE_MASKSUM 0
 #endif
+// 1: the ratio test's minimum as an exact DPP min plus a ballot for its lane; 0: a 6-bit lane tag
+// in the mantissa for the lane, then a DPP sum for the exact value (the earlier form)
+#ifndef WBC_T1_BALLOT
+#define WBC_T1_BALLOT 1
+#endif
 // ROWS: the J mirror already holds J0 by rows (rank6_factor); otherwise M = L^-1 (factor12)
 template <bool ROWS>
 __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, const Prob& P, UpdScratch& s) {
@@ -1359,9 +1364,16 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
             }
             // step: t1 (drop an active slot) or t2 (the new row becomes active)
             const double vt = (l < q && rk > 1e-14) ? u * fast_rcp(rk) : 1e300;
+#if WBC_T1_BALLOT
+            // the exact minimum (fmin returns one of its inputs), then its lowest lane from a
+            // ballot of the lanes that hold it: one 4-step DPP chain instead of two
+            const double t1 = seg16_min(vt);
+            const int l1 = __builtin_ctzll((__ballot(vt == t1) >> ((int)threadIdx.x & 48)) & 0xFFFFull);
+#else
             const double vtt = tag6(vt, l), vmin = seg16_min(vtt);
             const int l1 = untag6(vmin);
             const double t1 = seg_sum<16>((vtt == vmin) ? vt : 0.0);  // the exact value, DPP only
+#endif
             const double t2 = (zn > 1e-14) ? (-sps * fast_rcp(zn)) : 1e300;
             const double t = fmin(t1, t2);
             if (!(t < 1e299)) {
