@@ -12,18 +12,26 @@
 //   solveQP()                             hpp:54, cpp:466-542  -> wbc_solve
 //   computeJointTorques()                 hpp:52, cpp:553-577  -> wbc_get_output + publishers
 //   controlLoop()                         hpp:67, cpp:637-676  -> controlLoop(max_iterations, ...)
+//   run()                                 hpp:41, cpp:678-683  -> run(): control thread + spin
 //   terminate()                           hpp:69, cpp:627-636  -> publishes zero torques
 //
 // ROS is absent here: messages are plain structs with the same field names, and publishers are
-// std::function hooks.  The engine snapshots the inputs at updateState(), so the callbacks and
-// the control loop may run on different threads as long as each call is serialised by the caller
-// (the reference has no synchronisation at all, cpp:681-682).
+// std::function hooks.  The callbacks and the control cycle share the controller state under one
+// mutex: a cycle copies the callback state under the lock and runs the engine outside it, so the
+// callbacks may run on another thread (the reference shares that state with no synchronisation,
+// cpp:681-682, and snapshots only jointVel_, cpp:499).
+//
+// The reference node (src/whole_body_controller_node.cpp:6-7) builds unchanged against this
+// header: `WholeBodyController wbc; wbc.run();` (the class is also visible in the global
+// namespace, below; define WBC_NO_GLOBAL_ALIAS to keep it in wbc_mi355x only).
 #ifndef WBC_CONTROLLER_HPP
 #define WBC_CONTROLLER_HPP
 
 #include <array>
+#include <atomic>
 #include <cstdint>
 #include <functional>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -120,6 +128,21 @@ public:
     long controlLoop(long max_iterations, double rate_hz = 0.0,
                      const std::function<void(long)>& beforeCycle = nullptr);
 
+    // run() (hpp:41, cpp:678-683): starts controlLoop on its own thread (boost::thread at cpp:681)
+    // at params.loop_rate, and spins on the calling thread (ros::spin at cpp:682) until the loop
+    // ends: the QP fails (cpp:654-659) or requestShutdown() is called (ros::ok() turns false).
+    // While it spins it calls `spinOnce` repeatedly (the stand-in for ros::spin dispatching the
+    // subscriber callbacks; a host's message source calls the *Callback methods from there or from
+    // any other thread).  `loopHook(iteration)` runs on the control thread before every cycle.
+    // Returns the cycles run.  Errors on the control thread (an engine failure) are rethrown here.
+    long run();
+    void requestShutdown() { shutdown_.store(true); }
+    bool ok() const { return !shutdown_.load(); }
+    std::function<void()> spinOnce;
+    std::function<void(long)> loopHook;
+    // 0 runs the loop back to back (tests); default: params.loop_rate (400 Hz, cpp:639,673)
+    void setRunRate(double rate_hz) { runRate_ = rate_hz; }
+
     // publishers (cpp:41-43): jointTorquePub_, desiredGroundReactionForcesPub_
     std::function<void(const Float64MultiArray&)> jointTorquePublisher;
     std::function<void(const Float64MultiArray&)> desiredGroundReactionForcesPublisher;
@@ -134,8 +157,21 @@ public:
     wbc_engine* engine() { return engine_; }
 
 private:
+    struct Inputs {  // the callback state one cycle uses, copied under mu_
+        double basePose[WBC_POSE_LEN];
+        double nu[WBC_NU_LEN];
+        double jointPos[numberOfJoints];
+        double ref[WBC_REF_LEN];
+        uint8_t contacts;
+        uint8_t switching;
+    };
+    Inputs snapshot();
     void pushInputs();
     void publish();
+
+    std::mutex mu_;  // callbacks vs the control cycle's snapshot
+    std::atomic<bool> shutdown_{false};
+    double runRate_ = -1.0;  // < 0: params_.loop_rate
 
     wbc_engine* engine_ = nullptr;
     wbc_params params_{};
@@ -168,5 +204,10 @@ private:
 const std::array<std::string, numberOfJoints>& modelJointNames();
 
 }  // namespace wbc_mi355x
+
+#ifndef WBC_NO_GLOBAL_ALIAS
+// the name the reference node uses (src/whole_body_controller_node.cpp:6)
+using wbc_mi355x::WholeBodyController;
+#endif
 
 #endif  // WBC_CONTROLLER_HPP

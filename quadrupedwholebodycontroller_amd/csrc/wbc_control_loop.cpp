@@ -6,18 +6,25 @@
 //       BASELINE configs[0]: stance CoM-hold from the reference start-up pose (base 0.585 m, q0,
 //       all feet in contact, reference pose from params_controller.yaml), `cycles` (default 1000)
 //       control cycles; prints one JSON line with per-cycle latency and the last torques.
+//   wbc_control_loop run [cycles]
+//       the node's own entry, `WholeBodyController wbc; wbc.run();` (whole_body_controller_node.cpp:6-7):
+//       the control thread runs back to back while this thread spins, publishing the stance
+//       messages through the callbacks (ros::spin's role); a loop hook requests shutdown after
+//       `cycles` (default 200).  Prints one JSON line (cycles, QP status, torques, messages sent).
 //   wbc_control_loop replay <inputs.bin> <outputs.bin>
 //       feeds recorded per-cycle messages (tests/test_gpu_controller.py writes them from the golden
 //       trajectories) and writes status, iterations, tau and x per cycle.
 //       inputs.bin : int32 T, then T x (pose 7, nu 18, qj 12, ref 54, contacts, switching) doubles
 //       outputs.bin: T x (status, iters, tau 12, x 42) doubles
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "wbc_controller.hpp"
@@ -111,6 +118,40 @@ int run_stance(long cycles, double rate, uint32_t flags) {
     return wbc.qpReturnValue() == WBC_QP_OK ? 0 : 3;
 }
 
+int run_node(long cycles) {
+    WholeBodyController wbc;  // the node's two statements (whole_body_controller_node.cpp:6-7) ...
+    wbc.setRunRate(0.0);      // ... back to back instead of at 400 Hz
+    double pose[7] = {0.0, 0.0, 0.585, 0.0, 0.0, 0.0, 1.0};
+    double nu[18] = {0};
+    const double q0[12] = {0.0, -0.4, 0.8, 0.0, 0.4, -0.8, 0.0, 0.4, -0.8, 0.0, -0.4, 0.8};
+    wbc_params p;
+    wbc_default_params(&p);
+    double ref[54] = {0};
+    for (int i = 0; i < 6; ++i) ref[i] = p.initial_reference_pose[i];
+    const ModelStates ms = make_model_states(pose, nu);
+    const JointState js = make_joint_state(q0, nu + 6);
+    const WbcReferenceMsg rm = make_reference(ref, 15);
+    wbc.floatingBaseStateCallback(ms);  // locates the model (cpp:189-204)
+    std::atomic<long> sent{0};
+    wbc.spinOnce = [&]() {  // the subscriber callbacks, concurrently with the control thread
+        wbc.floatingBaseStateCallback(ms);
+        wbc.jointStateCallback(js);
+        wbc.referenceCallback(rm);
+        sent.fetch_add(1);
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+    };
+    wbc.loopHook = [&](long it) {
+        if (it + 1 >= cycles) wbc.requestShutdown();  // ros::shutdown: this cycle is the last
+    };
+    const long n = wbc.run();
+    const auto& tau = wbc.jointTorques();
+    std::printf("{\"config\": \"node_run\", \"cycles\": %ld, \"qp_status\": %d, \"messages\": %ld, \"tau\": [", n,
+                wbc.qpReturnValue(), sent.load());
+    for (int i = 0; i < numberOfJoints; ++i) std::printf("%s%.9g", i ? ", " : "", tau[i]);
+    std::printf("]}\n");
+    return wbc.qpReturnValue() == WBC_QP_OK ? 0 : 3;
+}
+
 int run_replay(const char* in_path, const char* out_path) {
     FILE* f = std::fopen(in_path, "rb");
     if (!f) throw std::runtime_error(std::string("cannot open ") + in_path);
@@ -170,7 +211,9 @@ int main(int argc, char** argv) {
                               (argc > 4 && std::string(argv[4]) == "fused") ? WBC_FUSED
                               : (argc > 4 && std::string(argv[4]) == "split") ? WBC_SPLIT : WBC_FUSED);
         if (mode == "replay" && argc > 3) return run_replay(argv[2], argv[3]);
-        std::fprintf(stderr, "usage: %s stance [cycles] [rate_hz] [fused|split] | replay <in.bin> <out.bin>\n", argv[0]);
+        if (mode == "run") return run_node(argc > 2 ? std::atol(argv[2]) : 200);
+        std::fprintf(stderr, "usage: %s stance [cycles] [rate_hz] [fused|split] | run [cycles] | replay <in.bin> <out.bin>\n",
+                     argv[0]);
         return 2;
     } catch (const std::exception& e) {
         std::fprintf(stderr, "wbc_control_loop: %s\n", e.what());

@@ -3,7 +3,9 @@
 #include "wbc_controller.hpp"
 
 #include <chrono>
+#include <climits>
 #include <cstring>
+#include <exception>
 #include <stdexcept>
 #include <thread>
 
@@ -40,6 +42,7 @@ WholeBodyController::~WholeBodyController() {
 void WholeBodyController::setInitialState() {
     // cpp:65-120: all feet in contact, identity attitude at z = 0.60, q0, zero velocities,
     // desiredPose_ = initialReferencePose, other references zero, history reset
+    std::lock_guard<std::mutex> lk(mu_);
     for (int i = 0; i < numberOfLegs; ++i) footContacts_[i] = 1;
     std::memset(basePose_, 0, sizeof(basePose_));
     basePose_[2] = 0.60;
@@ -55,6 +58,7 @@ void WholeBodyController::setInitialState() {
 
 void WholeBodyController::floatingBaseStateCallback(const ModelStates& msg) {
     // cpp:187-230: the first message only locates the model (and is otherwise ignored)
+    std::lock_guard<std::mutex> lk(mu_);
     if (firstFloatingBaseStateCallback_) {
         modelIndex_ = 0;
         while (modelIndex_ < (int)msg.name.size() && msg.name[modelIndex_] != modelName) ++modelIndex_;
@@ -74,6 +78,7 @@ void WholeBodyController::floatingBaseStateCallback(const ModelStates& msg) {
 
 void WholeBodyController::jointStateCallback(const JointState& msg) {
     // cpp:232-254: map message order to model order by name on the first message
+    std::lock_guard<std::mutex> lk(mu_);
     if (firstJointStateCallback_) {
         const auto& names = modelJointNames();
         for (int i = 0; i < numberOfJoints; ++i) {
@@ -96,9 +101,11 @@ void WholeBodyController::referenceCallback(const WbcReferenceMsg& m) {
                                      &m.desiredSwingLegsPosition, &m.desiredSwingLegsVelocity,
                                      &m.desiredSwingLegsAcceleration};
     const int n[6] = {6, 6, 6, 12, 12, 12};
+    for (int b = 0; b < 6; ++b)
+        if ((int)f[b]->data.size() < n[b]) throw std::invalid_argument("referenceCallback: short field");
+    std::lock_guard<std::mutex> lk(mu_);
     int off = 0;
     for (int b = 0; b < 6; ++b) {
-        if ((int)f[b]->data.size() < n[b]) throw std::invalid_argument("referenceCallback: short field");
         for (int i = 0; i < n[b]; ++i) ref_[off + i] = f[b]->data[i];
         off += n[b];
     }
@@ -110,12 +117,23 @@ void WholeBodyController::referenceCallback(const WbcReferenceMsg& m) {
     }
 }
 
+WholeBodyController::Inputs WholeBodyController::snapshot() {
+    std::lock_guard<std::mutex> lk(mu_);
+    Inputs in;
+    std::memcpy(in.basePose, basePose_, sizeof(basePose_));
+    std::memcpy(in.nu, nu_, sizeof(nu_));
+    std::memcpy(in.jointPos, jointPos_, sizeof(jointPos_));
+    std::memcpy(in.ref, ref_, sizeof(ref_));
+    in.contacts = 0;
+    for (int i = 0; i < numberOfLegs; ++i) in.contacts |= (uint8_t)(footContacts_[i] ? 1u << i : 0u);
+    in.switching = isSwitchingFootState_ ? 1 : 0;
+    return in;
+}
+
 void WholeBodyController::pushInputs() {
-    uint8_t contacts = 0;
-    for (int i = 0; i < numberOfLegs; ++i) contacts |= (uint8_t)(footContacts_[i] ? 1u << i : 0u);
-    const uint8_t sw = isSwitchingFootState_ ? 1 : 0;
-    check(wbc_set_state(engine_, basePose_, nu_, jointPos_), "wbc_set_state");
-    check(wbc_set_reference(engine_, ref_, &contacts, &sw), "wbc_set_reference");
+    const Inputs in = snapshot();
+    check(wbc_set_state(engine_, in.basePose, in.nu, in.jointPos), "wbc_set_state");
+    check(wbc_set_reference(engine_, in.ref, &in.contacts, &in.switching), "wbc_set_reference");
 }
 
 void WholeBodyController::updateState() {
@@ -139,12 +157,10 @@ void WholeBodyController::computeJointTorques() {
 }
 
 void WholeBodyController::controlCycle() {
-    uint8_t contacts = 0;
-    for (int i = 0; i < numberOfLegs; ++i) contacts |= (uint8_t)(footContacts_[i] ? 1u << i : 0u);
-    const uint8_t sw = isSwitchingFootState_ ? 1 : 0;
+    const Inputs in = snapshot();  // the callbacks may keep running while the engine steps
     int32_t st = 0, it = 0;
-    check(wbc_cycle(engine_, basePose_, nu_, jointPos_, ref_, &contacts, &sw, stepFlags_, tau_.data(), grf_.data(), x_.data(),
-                    &st, &it),
+    check(wbc_cycle(engine_, in.basePose, in.nu, in.jointPos, in.ref, &in.contacts, &in.switching, stepFlags_, tau_.data(),
+                    grf_.data(), x_.data(), &st, &it),
           "wbc_cycle");
     firstControllerIteration_ = false;
     qpStatus_ = st;
@@ -182,7 +198,7 @@ long WholeBodyController::controlLoop(long max_iterations, double rate_hz, const
     const auto period = rate_hz > 0 ? std::chrono::duration<double>(1.0 / rate_hz) : std::chrono::duration<double>(0);
     auto next = std::chrono::steady_clock::now();
     long iteration = 0;
-    for (; iteration < max_iterations; ++iteration) {
+    for (; iteration < max_iterations && ok(); ++iteration) {  // while (ros::ok()) (cpp:648)
         if (beforeCycle) beforeCycle(iteration);
         controlCycle();  // updateState(); solveQP(); computeJointTorques();
         if (qpStatus_ != WBC_QP_OK) {  // cpp:654-659
@@ -196,6 +212,39 @@ long WholeBodyController::controlLoop(long max_iterations, double rate_hz, const
         }
     }
     return iteration;
+}
+
+long WholeBodyController::run() {
+    // cpp:678-683: the control loop on its own thread, the callbacks on this one (ros::spin)
+    shutdown_.store(false);
+    std::atomic<bool> finished{false};
+    std::exception_ptr err;
+    long cycles = 0;
+    const double rate = runRate_ < 0.0 ? params_.loop_rate : runRate_;
+    std::thread ctrl([&]() {
+        try {
+            cycles = controlLoop(LONG_MAX, rate, loopHook);
+        } catch (...) {
+            err = std::current_exception();
+        }
+        finished.store(true);
+    });
+    while (!finished.load()) {  // ros::spin(): returns once the node shuts down
+        if (spinOnce) {
+            try {
+                spinOnce();
+            } catch (...) {
+                requestShutdown();
+                ctrl.join();
+                throw;
+            }
+        } else {
+            std::this_thread::sleep_for(std::chrono::microseconds(200));
+        }
+    }
+    ctrl.join();
+    if (err) std::rethrow_exception(err);
+    return cycles;
 }
 
 }  // namespace wbc_mi355x

@@ -71,7 +71,7 @@ struct wbc_engine {
     double* d_hist = nullptr;
     double* d_work = nullptr;
     int32_t* d_fb = nullptr;  // elimination fallback counters [2] + list [B] (KernelArgs::fb)
-    int32_t parity = 0;       // fallback counter of the next update
+    int32_t parity = 0;       // fallback counter of the next elimination update
     // four-contact rows among the engine's own contact masks (d_contacts, as last copied from the
     // host) and among the mode masks: the stance elimination runs when every QP of a step has
     // mask 15 (known only for the engine's own masks; device-bound masks take the general path)
@@ -94,6 +94,10 @@ struct wbc_engine {
     bool updated = false;
     bool timed = false;    // a WBC_TIMED step has recorded ev0 / ev1
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // last launch on a caller's stream (wbc_set_stream): the engine waits for this event, not for
+    // the stream (which the caller may destroy) or the device (other engines' and torch's work)
+    hipEvent_t done_ev = nullptr;
+    bool done_pending = false;
     double last_ms = 0.0;
 };
 
@@ -142,7 +146,24 @@ wbc::KernelArgs make_args(wbc_engine* h, uint32_t flags) {
     a.elim = 0;
     a.parity = 0;
     a.fb = h->d_fb;
+    a.fb_cap = h->batch;
     return a;
+}
+
+// after the launches of an API call: on a caller's stream, remember where they end
+hipError_t note_launch(wbc_engine* h) {
+    if (h->stream == h->own_stream) return hipSuccess;
+    h->done_pending = true;
+    return hipEventRecord(h->done_ev, h->stream);
+}
+
+// wait for every launch the engine queued so far (its own stream, or the caller's up to done_ev)
+hipError_t drain(wbc_engine* h) {
+    if (h->stream == h->own_stream) return h->own_stream ? hipStreamSynchronize(h->own_stream) : hipSuccess;
+    if (!h->done_pending) return hipSuccess;
+    const hipError_t e = hipEventSynchronize(h->done_ev);
+    if (e == hipSuccess) h->done_pending = false;
+    return e;
 }
 
 int64_t count_stance(const uint8_t* masks, size_t n) {
@@ -159,17 +180,14 @@ void begin_update(wbc_engine* h, wbc::KernelArgs& a) {
     if (h->n_modes) all = h->modes_stance == h->n_modes;
     else if (h->in_contacts == h->d_contacts) all = h->n_stance_own == h->batch;
     h->elim = all && wbc_kernel_stance_elim();
+    // the fallback counters alternate between elimination updates only: the update with parity p
+    // fills fb[p] and clears fb[p ^ 1], which only the next elimination update uses (an update
+    // without the elimination neither fills nor clears a list, so it must not move the parity)
     h->elim_parity = h->parity;
-    h->parity ^= 1;
+    if (h->elim) h->parity ^= 1;
     a.elim = h->elim ? 1 : 0;
     a.parity = h->elim_parity;
 }
-
-// Stateless all-stance wbc_step: update and stance solve in one kernel (wbc_update_solve_kernel);
-// 0 keeps the separate stance solve kernel (A/B builds)
-#ifndef WBC_INLINE_STANCE
-#define WBC_INLINE_STANCE 1
-#endif
 
 hipError_t launch_solves(wbc_engine* h, wbc::KernelArgs& a) {
     a.elim = h->elim ? 1 : 0;
@@ -261,7 +279,8 @@ int32_t wbc_create(const wbc_model* model, const wbc_params* params, int32_t bat
     ALLOC(d_dbg, B * WBC_DBG_LEN);
 #undef ALLOC
     if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) {
+        hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess ||
+        hipEventCreateWithFlags(&h->done_ev, hipEventDisableTiming) != hipSuccess) {
         wbc_destroy(h);
         return fail(WBC_ERR_HIP, "stream/event creation failed");
     }
@@ -305,9 +324,10 @@ int32_t wbc_create(const wbc_model* model, const wbc_params* params, int32_t bat
 int32_t wbc_destroy(wbc_engine* h) {
     if (!h) return WBC_OK;
     (void)hipSetDevice(h->device);
-    // drain in-flight work before freeing: the device, not h->stream, which may be a caller's
-    // stream that was already destroyed
-    (void)hipDeviceSynchronize();
+    // drain the engine's in-flight work before freeing: its own stream, or the event recorded
+    // after its last launch on a caller's stream (which may be destroyed by now); never the whole
+    // device, which would also wait for other engines' and the caller's unrelated work
+    (void)drain(h);
     void* ptrs[] = {h->d_model, h->d_params, h->d_inblk, h->d_outblk, h->d_mask, h->d_modes, h->d_hist, h->d_work,
                     h->d_fb, h->d_dbg};
     for (void* p : ptrs)
@@ -316,6 +336,7 @@ int32_t wbc_destroy(wbc_engine* h) {
     if (h->h_out) (void)hipHostFree(h->h_out);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
+    if (h->done_ev) (void)hipEventDestroy(h->done_ev);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
     return WBC_OK;
@@ -328,11 +349,13 @@ int32_t wbc_set_stream(wbc_engine* h, void* stream) {
     const hipStream_t next = stream ? reinterpret_cast<hipStream_t>(stream) : h->own_stream;
     if (next != h->stream) {
         // work already queued on the old stream still reads the engine's buffers: let it finish
-        // before any call on the new stream can overwrite them
+        // before any call on the new stream can overwrite them (through the event after its last
+        // launch when the old stream is a caller's, so a caller stream destroyed since is safe)
         WBC_HIP(hipSetDevice(h->device));
-        WBC_HIP(hipStreamSynchronize(h->stream));
+        WBC_HIP(drain(h));
     }
     h->stream = next;
+    h->done_pending = false;
     return WBC_OK;
 }
 
@@ -395,6 +418,7 @@ int32_t wbc_reset(wbc_engine* h, const uint8_t* mask) {
     }
     WBC_HIP(wbc_launch_reset(h->d_hist, dm, h->batch, h->stream));
     WBC_HIP(hipStreamSynchronize(h->stream));
+    h->done_pending = false;
     h->updated = false;
     return WBC_OK;
 }
@@ -406,6 +430,7 @@ int32_t wbc_update(wbc_engine* h, uint32_t flags) {
     wbc::KernelArgs a = make_args(h, flags);
     begin_update(h, a);
     WBC_HIP(wbc_launch_update(&a, h->stream));
+    WBC_HIP(note_launch(h));
     h->updated = true;
     return WBC_OK;
 }
@@ -417,6 +442,7 @@ int32_t wbc_solve(wbc_engine* h, uint32_t flags) {
     WBC_HIP(hipSetDevice(h->device));
     wbc::KernelArgs a = make_args(h, flags);
     WBC_HIP(launch_solves(h, a));
+    WBC_HIP(note_launch(h));
     return WBC_OK;  // the assembled problem stays valid: solving it again gives the same result
 }
 
@@ -431,7 +457,7 @@ int32_t wbc_step(wbc_engine* h, uint32_t flags) {
     const bool split = (flags & WBC_SPLIT) || (!(flags & WBC_FUSED) && wbc_kernel_default_split());
     if (split) {
         begin_update(h, a);
-        if (h->elim && !a.stateful && WBC_INLINE_STANCE) {
+        if (h->elim && !a.stateful) {
             // stateless all-stance step: the update kernel solves the stance QPs itself
             WBC_HIP(wbc_launch_update_solve(&a, h->stream));
         } else {
@@ -445,6 +471,7 @@ int32_t wbc_step(wbc_engine* h, uint32_t flags) {
         WBC_HIP(hipEventRecord(h->ev1, h->stream));
         h->timed = true;
     }
+    WBC_HIP(note_launch(h));
     h->updated = false;
     return WBC_OK;
 }
@@ -486,6 +513,7 @@ int32_t wbc_step_modes(wbc_engine* h, uint32_t flags) {
         WBC_HIP(hipEventRecord(h->ev1, h->stream));
         h->timed = true;
     }
+    WBC_HIP(note_launch(h));
     h->updated = false;
     return WBC_OK;
 }
@@ -514,9 +542,9 @@ int32_t wbc_cycle(wbc_engine* h, const double* base_pose, const double* nu, cons
     std::memcpy(hp, ref, B * WBC_REF_LEN * sizeof(double));
     hp += B * WBC_REF_LEN;
     std::memcpy(reinterpret_cast<uint8_t*>(hp), contacts, B);
-    h->n_stance_own = count_stance(contacts, B);
     std::memcpy(reinterpret_cast<uint8_t*>(hp) + B, switching, B);
     WBC_HIP(hipMemcpyAsync(h->d_inblk, h->h_in, inb, hipMemcpyHostToDevice, h->stream));
+    h->n_stance_own = count_stance(contacts, B);  // d_contacts holds these masks from here on
     // inputs from the engine's own block for this step only (caller bindings are restored after)
     const double* const ip = h->in_pose; const double* const in = h->in_nu; const double* const iq = h->in_qj;
     const double* const ir = h->in_ref; const uint8_t* const ic = h->in_contacts; const uint8_t* const is = h->in_switching;

@@ -176,13 +176,10 @@ __device__ __forceinline__ double vbcast(double v, int lane) {
 // row_newbcast): v_mov_b32_dpp without an "old" operand (update_dpp(0, ...) makes the compiler
 // zero the destination first, one extra move per 32-bit half)
 // row_newbcast (0x150 + lane) is the one pattern gfx950 allows on 64-bit DPP: one v_mov_b64_dpp
-// instead of two v_mov_b32_dpp (WBC_DPP64=0 keeps the 32-bit pair, the earlier form)
-#ifndef WBC_DPP64
-#define WBC_DPP64 1
-#endif
+// instead of two v_mov_b32_dpp
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double v) {
-    if constexpr (WBC_DPP64 && CTRL >= 0x150 && CTRL <= 0x15F) {
+    if constexpr (CTRL >= 0x150 && CTRL <= 0x15F) {
         const long long b = __builtin_bit_cast(long long, v);
         const long long r = __builtin_amdgcn_mov_dpp(b, CTRL, 0xF, 0xF, false);
         return __builtin_bit_cast(double, r);
@@ -326,47 +323,10 @@ __device__ __forceinline__ bool seg_any(bool p) {
     }
 }
 
-// XCD-aware robot index (optional, -DWBC_XCD_REMAP=1).  Workgroups are dealt round-robin to the
-// 8 XCDs (blockIdx % 8), each with its own L2; the remap gives every XCD a contiguous range of
-// robots so that robot-major rows sharing a cache line stay on one XCD.  Measured on MI355X
-// (profiles/r01/variants_xcd_remap.log): HBM traffic per launch 15.1 -> 11.4 MB but the kernel
-// 14 % slower for B = 4096 stance, so it is off by default.  Bijective for any grid size.
-#ifndef WBC_EQ_BCAST_LDS
-#define WBC_EQ_BCAST_LDS 0
-#endif
-#ifndef WBC_EQ_BPERM
-#define WBC_EQ_BPERM 0
-#endif
-// Drop in the active-set loop: 1 = Givens deletion (the remaining slots' R columns and every
-// constraint column rotated in place, R^-1 updated by the same rotations), 0 = restart from the
-// initial columns C0 and re-add the remaining active set
-#ifndef WBC_GIVENS_DROP
-#define WBC_GIVENS_DROP 1
-#endif
-#ifndef WBC_LOOP_BPERM
-#define WBC_LOOP_BPERM 1  // measured: B = 4096 stance 100.5 -> 95.4 us, rl_random B = 8192 453 -> 376 us (profiles/r01/variants_loop_bperm.log)
-#endif
-#ifndef WBC_XCD_REMAP
-#define WBC_XCD_REMAP 0
-#endif
-// Four-contact stance solved in the 12-variable force space (Presolve::stance, wbc_layout.h)
-#ifndef WBC_STANCE_ELIM
-#define WBC_STANCE_ELIM 1
-#endif
-// Inline solve's force-space factor: 1 = rank-6 form (rank6_factor), 0 = 12 x 12 Cholesky (factor12)
-#ifndef WBC_RANK6
-#define WBC_RANK6 1
-#endif
-#ifndef WBC_STANCE_KERNEL
-#define WBC_STANCE_KERNEL 1  // 1: stance QPs in wbc_solve_stance_kernel (+ fallback kernel); 0: in wbc_solve_kernel
-#endif
-__device__ __forceinline__ int xcd_robot() {
-    if (!WBC_XCD_REMAP) return blockIdx.x;
-    constexpr int NXCD = 8;
-    const int n = gridDim.x, b = blockIdx.x;
-    const int x = b % NXCD, i = b / NXCD, full = n / NXCD, rem = n % NXCD;
-    return x * full + (x < rem ? x : rem) + i;
-}
+// One workgroup per robot: blockIdx -> robot.  (An XCD-aware remap, giving each XCD a contiguous
+// robot range so that robot-major rows sharing a cache line stay in one L2, cut HBM traffic per
+// launch 15.1 -> 11.4 MB but made the kernel 14 % slower at B = 4096, profiles/r01/variants_xcd_remap.log.)
+__device__ __forceinline__ int xcd_robot() { return blockIdx.x; }
 
 // ---------------------------------------------------------------------------------------
 // small fp64 linear algebra (row-major 3x3)
@@ -861,7 +821,7 @@ __device__ bool stance_reduce([[maybe_unused]] const KernelArgs& ka, [[maybe_unu
     // H_f row i = e_i + E H^ E_i^T: h = H^ E_i^T, then E_j . h = h[k_j] - (d_{l_j} x h_ang)[k_j]
     // (not needed by the inline solve's rank-6 factor)
     {
-        if constexpr (!(SOLVE && WBC_RANK6)) {
+        if constexpr (!SOLVE) {
         double h[6];
 #pragma unroll
         for (int ra = 0; ra < 6; ++ra) {
@@ -945,7 +905,7 @@ __device__ bool stance_reduce([[maybe_unused]] const KernelArgs& ka, [[maybe_unu
 }
 
 // ---------------------------------------------------------------------------------------
-// Force-space factor for the inline solve without a 12-step Cholesky (WBC_RANK6).  H_f = I + E Ĥ Eᵀ
+// Force-space factor for the inline solve without a 12-step Cholesky.  H_f = I + E Ĥ Eᵀ
 // is the identity plus rank 6 (E = stacked [I, -S(d_l)], 12 x 6), and the dual method needs only
 // some J0 with J0 J0ᵀ = H_f⁻¹ (its iterates do not depend on which).  With EᵀE = L_G L_Gᵀ and
 // Q = E L_G⁻ᵀ (orthonormal columns), H_f = (I - QQᵀ) + Q (I + B) Qᵀ for B = L_Gᵀ Ĥ L_G, so with
@@ -1195,15 +1155,6 @@ __device__ __forceinline__ int seg_shfl_i(int v, int j) {
 }
 __device__ __forceinline__ double sel3d(int j, double a, double b, double c) { return j == 0 ? a : (j == 1 ? b : c); }
 
-// 1: d[pos] and J[l][pos] as 12-term sums against a row mask (the form before round 2's A/B)
-#ifndef WBC_INLINE_MASKSUM
-#define WBC_INLINE_MASKSUM 0
-#endif
-// 1: the ratio test's minimum as an exact DPP min plus a ballot for its lane; 0: a 6-bit lane tag
-// in the mantissa for the lane, then a DPP sum for the exact value (the earlier form)
-#ifndef WBC_T1_BALLOT
-#define WBC_T1_BALLOT 1
-#endif
 // ROWS: the J mirror already holds J0 by rows (rank6_factor); otherwise M = L^-1 (factor12)
 template <bool ROWS>
 __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, const Prob& P, UpdScratch& s) {
@@ -1319,34 +1270,28 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
             // d[pos] and J[l][pos] (needed only by the Householder add, so their LDS latency is
             // off the chain): from lane pos of the segment and from the J mirror, instead of
             // 12-term sums against a 0 / 1 row mask (pos varies by segment)
-            const double dq = WBC_INLINE_MASKSUM ? 0.0 : seg_shfl(dj, pos);  // lane 12.. holds 0
-            const double jqm = (WBC_INLINE_MASKSUM || l >= N || pos >= N) ? 0.0 : Jl[i * 12 + (pos < N ? pos : 0)];
-            double rk, zn, dqs;
+            const double dq = seg_shfl(dj, pos);  // lane 12.. holds 0
+            const double jq = (l >= N || pos >= N) ? 0.0 : Jl[i * 12 + (pos < N ? pos : 0)];
+            double rk, zn;
             {
-                double acc[4] = {0.0, 0.0, 0.0, 0.0}, zz[4] = {0, 0, 0, 0}, ee[4] = {0, 0, 0, 0};
+                double acc[4] = {0.0, 0.0, 0.0, 0.0}, zz[4] = {0, 0, 0, 0};
 #pragma unroll
                 for (int j = 0; j < N; ++j) {
                     const double mk = (j >= pos) ? 1.0 : 0.0;
                     acc[j & 3] += rinv[j] * d[j];
                     d2[j] = d[j] * mk;
                     zz[j & 3] += d[j] * d2[j];
-                    if (WBC_INLINE_MASKSUM) ee[j & 3] += d[j] * ((j == pos) ? 1.0 : 0.0);
                 }
                 rk = (l < N) ? (acc[0] + acc[1]) + (acc[2] + acc[3]) : 0.0;
                 zn = (zz[0] + zz[1]) + (zz[2] + zz[3]);
-                dqs = WBC_INLINE_MASKSUM ? (ee[0] + ee[1]) + (ee[2] + ee[3]) : dq;
             }
             // primal direction z = J2 d2 (lane k: z_k), then to every lane; slack rates n . z
-            double zk, jq;
+            double zk;
             {
-                double acc[4] = {0.0, 0.0, 0.0, 0.0}, e4[4] = {0.0, 0.0, 0.0, 0.0};
+                double acc[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-                for (int j = 0; j < N; ++j) {
-                    acc[j & 3] += Jr[j] * d2[j];
-                    if (WBC_INLINE_MASKSUM) e4[j & 3] += Jr[j] * ((j == pos) ? 1.0 : 0.0);
-                }
+                for (int j = 0; j < N; ++j) acc[j & 3] += Jr[j] * d2[j];
                 zk = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-                jq = WBC_INLINE_MASKSUM ? (e4[0] + e4[1]) + (e4[2] + e4[3]) : jqm;
             }
             double cz0, cz1, cz2;
             {
@@ -1364,16 +1309,11 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
             }
             // step: t1 (drop an active slot) or t2 (the new row becomes active)
             const double vt = (l < q && rk > 1e-14) ? u * fast_rcp(rk) : 1e300;
-#if WBC_T1_BALLOT
             // the exact minimum (fmin returns one of its inputs), then its lowest lane from a
-            // ballot of the lanes that hold it: one 4-step DPP chain instead of two
+            // ballot of the lanes that hold it (one 4-step DPP chain; a 6-bit lane tag in the
+            // mantissa needed a second chain to recover the exact value)
             const double t1 = seg16_min(vt);
             const int l1 = __builtin_ctzll((__ballot(vt == t1) >> ((int)threadIdx.x & 48)) & 0xFFFFull);
-#else
-            const double vtt = tag6(vt, l), vmin = seg16_min(vtt);
-            const int l1 = untag6(vmin);
-            const double t1 = seg_sum<16>((vtt == vmin) ? vt : 0.0);  // the exact value, DPP only
-#endif
             const double t2 = (zn > 1e-14) ? (-sps * fast_rcp(zn)) : 1e300;
             const double t = fmin(t1, t2);
             if (!(t < 1e299)) {
@@ -1393,24 +1333,18 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
                     // R^-1 gains the column [-r / alpha; 1 / alpha]
                     const double rs = fast_rsq(zn);
                     const double nrm2 = zn * rs;
-                    const double alpha = (dqs >= 0.0) ? -nrm2 : nrm2;
-                    const double ia = (dqs >= 0.0) ? -rs : rs;
-                    const double beta = fast_rcp(zn + nrm2 * fabs(dqs));
+                    const double alpha = (dq >= 0.0) ? -nrm2 : nrm2;
+                    const double ia = (dq >= 0.0) ? -rs : rs;
+                    const double beta = fast_rcp(zn + nrm2 * fabs(dq));
                     const double vw = (zk - alpha * jq) * beta, vwa = vw * alpha;
 #pragma unroll
                     for (int k = 0; k < N; ++k) Jr[k] = fma(vwa, (k == pos) ? 1.0 : 0.0, fma(-vw, d2[k], Jr[k]));
                     const double nv = (l == pos) ? ia : -rk * ia;
-                    const bool wcol = l <= pos;
-                    if (WBC_INLINE_MASKSUM) {
+                    // column pos of R^-1 is 0 before the add and nv is finite here (zn > 1e-14),
+                    // so adding nv under the 0 / 1 mask is exact
+                    const double nvw = (l <= pos) ? nv : 0.0;
 #pragma unroll
-                        for (int k = 0; k < N; ++k) rinv[k] = (wcol && k == pos) ? nv : rinv[k];
-                    } else {
-                        // column pos of R^-1 is 0 before the add and nv is finite here (zn > 1e-14),
-                        // so adding nv under the 0 / 1 mask is exact
-                        const double nvw = wcol ? nv : 0.0;
-#pragma unroll
-                        for (int k = 0; k < N; ++k) rinv[k] = fma((k == pos) ? 1.0 : 0.0, nvw, rinv[k]);
-                    }
+                    for (int k = 0; k < N; ++k) rinv[k] = fma((k == pos) ? 1.0 : 0.0, nvw, rinv[k]);
                 } else {
                     // drop slot l1: shift the active lists, then Givens deletion (givens_drop) with the
                     // rotation of step k from the R column of the row now in slot k: (J^T n)[k, k+1]
@@ -2151,12 +2085,12 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
         double hrow[12], gsv = 0.0;
         bool stance = false;
         if constexpr (SUB == 16) {
-            if (WBC_STANCE_ELIM && a.elim && (kap == 15 || a.modes))
+            if (a.elim && (kap == 15 || a.modes))
                 stance = stance_reduce<SOLVE>(a, rb, P, pr, lane, wr, s, hrow, gsv, pre);
         }
         const bool fact = stance || !a.modes;
         if (fact) {
-            if constexpr (SOLVE && SUB == 16 && WBC_RANK6) {
+            if constexpr (SOLVE && SUB == 16) {
                 if (stance) {
                     if (rank6_factor(P, s, gsv, lane)) {
                         UST(a, rb, 11);
@@ -2169,13 +2103,6 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
             if (!stance) slot_hessian_row(P, kap, pr, lane, hrow, gsv);
             const bool ok = factor12<SUB>(hrow, gsv, lane, s.ps.L, s.ps.ild, s.ps.xs, &a, rb);
             const double (&Mi)[12][12] = *reinterpret_cast<const double(*)[12][12]>(&s.ps.L[0][0]);
-            if constexpr (SOLVE && SUB == 16 && !WBC_RANK6) {
-                if (stance && ok) {
-                    UST(a, rb, 11);
-                    solve_stance16<false>(a, rb, lane, wr, P, s);
-                    return true;
-                }
-            }
             if (wr) {
                 for (int k = lane; k < 78; k += SUB) {
                     const int i = (int)((sqrt(8.0 * k + 1.0) - 1.0) * 0.5);
@@ -2332,7 +2259,7 @@ __device__ __forceinline__ void to_column(QpScratch& s, double* cc) {
 template <int N>
 __device__ __forceinline__ void read_column(const double* cc, int p, double* d) {
 #pragma unroll
-    for (int k = 0; k < N; ++k) d[k] = WBC_LOOP_BPERM ? vbcast(cc[k], p) : bcast(cc[k], p);
+    for (int k = 0; k < N; ++k) d[k] = vbcast(cc[k], p);  // ds_bpermute: 100.5 -> 95.4 us vs v_readlane (profiles/r01/variants_loop_bperm.log)
 }
 template <class S>
 __device__ __forceinline__ void zero_rinv(S& s) {
@@ -2626,21 +2553,8 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, const Pr
             if (e < mp.neq && q == e) {
                 const double zn = bcast(tn, e);
                 double d[NQ];
-#if WBC_EQ_BCAST_LDS
-                // column broadcast through LDS: lane e writes rows e.., every lane reads them back
-                // (LDS instructions instead of 2 (24 - e) v_readlane on the VALU)
-                if (lane == e) {
 #pragma unroll
-                    for (int k = e & ~1; k < NQ; ++k) s.colbuf[k] = cc[k];
-                }
-                lds_sync();
-#pragma unroll
-                for (int k = 0; k < NQ; ++k) d[k] = (k >= e) ? s.colbuf[k] : 0.0;
-                lds_sync();
-#else
-#pragma unroll
-                for (int k = 0; k < NQ; ++k) d[k] = (k >= e) ? (WBC_EQ_BPERM ? vbcast(cc[k], e) : bcast(cc[k], e)) : 0.0;
-#endif
+                for (int k = 0; k < NQ; ++k) d[k] = (k >= e) ? bcast(cc[k], e) : 0.0;
                 const bool add = !(zn <= tiny * fmax(1.0, bcast(nn, e)));
                 // Householder reflection on rows e..23 (static q = e)
                 {
@@ -2944,21 +2858,9 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, const Pr
             }
             lds_sync();
         }
-        if (drop && WBC_GIVENS_DROP) {
+        if (drop) {
             givens_drop(s, drop_slot, q, act, cc);
             lds_sync();
-        } else if (drop) {
-            // C restarts from C0 and the remaining active set is re-added (rebuild mode).
-            const int pl = lane < C0_LANES ? lane : 0;
-#pragma unroll
-            for (int k = 0; k < NQ; k += 2) {  // fresh C0 (stored at the start); slacks sp are kept
-                const double2 c = s.c0[k / 2][pl];
-                cc[k] = lane < C0_LANES ? c.x : 0.0;
-                cc[k + 1] = lane < C0_LANES ? c.y : 0.0;
-            }
-            zero_rinv(s);
-            lds_sync();
-            rbk = 0;
         }
         IST(5);  // bookkeeping, barrier, drop path
     }
@@ -3415,26 +3317,15 @@ __device__ void solve_stance(const KernelArgs& a, int rb, const Prob* Pg, const 
 // ---------------------------------------------------------------------------------------
 #define WBC_KERNEL_ATTR \
     __global__ __attribute__((amdgpu_flat_work_group_size(64, 64), amdgpu_waves_per_eu(WBC_WAVES_PER_SIMD)))
-// Split-mode update kernel: WBC_UPDATE_SUB lanes per robot, 64 / SUB robots per wave.  16 (four
-// robots per wave) is the default: the update phase keeps at most 13 lanes of a robot busy, so a
-// 64-lane robot wastes 3/4 of every VALU issue.  Four robots' scratch (36 KB of LDS per
-// workgroup) limits the kernel to one wave per SIMD; measured on MI355X it still beats the
-// one-robot-per-wave update (which runs at 2 waves per SIMD) and the fused kernel: B = 4096
-// stance 110.0 -> 100.3 us per step, B = 16384 342 -> 310 us (profiles/r01/variants_update_sub.log).
-#ifndef WBC_UPDATE_SUB
-#define WBC_UPDATE_SUB 16
-#endif
-#ifndef WBC_UPDATE_WAVES_PER_SIMD
-#define WBC_UPDATE_WAVES_PER_SIMD (WBC_UPDATE_SUB == 16 ? 1 : 2)
-#endif
+// Split-mode update kernel: 16 lanes per robot, four robots per wave: the update phase keeps at
+// most 13 lanes of a robot busy, so a 64-lane robot wastes 3/4 of every VALU issue.  Four robots'
+// scratch (≈ 39 KB of LDS per workgroup) limits the kernel to one wave per SIMD; measured on
+// MI355X it still beats the one-robot-per-wave update (which runs at 2 waves per SIMD) and the
+// fused kernel: B = 4096 stance 110.0 -> 100.3 us per step, B = 16384 342 -> 310 us
+// (profiles/r01/variants_update_sub.log).
 #define WBC_UPDATE_KERNEL_ATTR \
-    __global__ __attribute__((amdgpu_flat_work_group_size(64, 64), amdgpu_waves_per_eu(WBC_UPDATE_WAVES_PER_SIMD)))
-// wbc_step's default form: 1 = update kernel + solve kernel (the problem passes through HBM,
-// 2.9 KB per robot each way), 0 = the fused kernel
-#ifndef WBC_DEFAULT_SPLIT
-#define WBC_DEFAULT_SPLIT 1
-#endif
-constexpr int UPD_SUB = WBC_UPDATE_SUB, UPD_RPW = 64 / UPD_SUB;
+    __global__ __attribute__((amdgpu_flat_work_group_size(64, 64), amdgpu_waves_per_eu(1)))
+constexpr int UPD_SUB = 16, UPD_RPW = 64 / UPD_SUB;
 struct UpdLds {
     wbc_model model;  // staged once per wave: the kinematic chain reads it at lane-varying addresses
     Prob prob[UPD_RPW];
@@ -3442,10 +3333,7 @@ struct UpdLds {
 };
 struct SolveLds {
     Prob prob;
-    union {
-        QpScratch q;
-        StanceScratch st;  // the combined form (WBC_STANCE_KERNEL 0): stance QPs in this kernel
-    };
+    QpScratch q;
 };
 
 WBC_KERNEL_ATTR void wbc_step_kernel(KernelArgs a) {
@@ -3506,14 +3394,8 @@ __device__ __forceinline__ void stage_to_lds(double2* dst, const double2* src, i
 template <bool SOLVE>
 __device__ __forceinline__ void update_kernel_body(const KernelArgs& a) {
     __shared__ UpdLds L;
-    int seg, lane, rb;
-    if constexpr (UPD_SUB == 64) {
-        seg = 0; lane = lane_id(); rb = xcd_robot();
-        if (rb >= a.batch) return;
-    } else {
-        seg = (int)threadIdx.x / UPD_SUB; lane = (int)threadIdx.x % UPD_SUB;
-        rb = (int)blockIdx.x * UPD_RPW + seg;
-    }
+    const int seg = (int)threadIdx.x / UPD_SUB, lane = (int)threadIdx.x % UPD_SUB;
+    int rb = (int)blockIdx.x * UPD_RPW + seg;
     const bool wr = rb < a.batch;  // a padding segment recomputes the last robot, writes nothing
     if (!wr) rb = a.batch - 1;
     stage_to_lds<(int)(sizeof(wbc_model) / 8)>(reinterpret_cast<double*>(&L.model),
@@ -3528,19 +3410,19 @@ __device__ __forceinline__ void update_kernel_body(const KernelArgs& a) {
     if (wr && !(SOLVE && stance)) {
         for (int k = lane; k < PROB_LEN / 2; k += UPD_SUB) dst[k] = src[k];
     }
-    // mask-15 QPs whose elimination failed go to the fallback list (rare: one atomic each)
-    if (WBC_STANCE_ELIM && a.elim && wr && !stance) {
+    // QPs whose elimination did not happen go to the fallback list (rare: one atomic each): every
+    // one of them, whatever its mask, so that a wrong host decision (a mask the host counted as 15)
+    // costs speed, never a QP left unsolved
+    if (a.elim && wr && !stance) {
         const int K = a.modes;
-        const bool mine = K ? (lane < K && (a.mode_masks[lane < K ? lane : 0] & 15) == 15)
-                            : (lane == 0 && (a.contacts[rb] & 15) == 15);
-        if (mine) {
+        if (K ? lane < K : lane == 0) {
             const int idx = atomicAdd(&a.fb[a.parity], 1);
-            a.fb[2 + idx] = K ? rb * K + lane : rb;
+            if (idx < a.fb_cap) a.fb[2 + idx] = K ? rb * K + lane : rb;
         }
     }
 }
 WBC_UPDATE_KERNEL_ATTR void wbc_update_kernel(KernelArgs a) { update_kernel_body<false>(a); }
-WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) { update_kernel_body<WBC_STANCE_ELIM != 0>(a); }
+WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) { update_kernel_body<true>(a); }
 
 // Four-contact QP whose equalities the update kernel eliminated (its Presolve::stance flag, in
 // the record registers): wbc_solve_stance_kernel's; every other QP is wbc_solve_kernel's.
@@ -3554,20 +3436,6 @@ WBC_KERNEL_ATTR void wbc_solve_kernel(KernelArgs a) {
     __shared__ SolveLds L;
     const int rb = xcd_robot();
     if (rb >= a.batch) return;
-    if (!WBC_STANCE_KERNEL && WBC_STANCE_ELIM && a.elim) {
-        // combined form: a step with the elimination on is all mask 15 (bar mode hypotheses), so
-        // waiting for the record flag before the problem copy costs the rare general QP only
-        const int row = a.modes ? rb / a.modes : rb;
-        const double* prow = a.work + (size_t)row * WORK_LEN + PROB_LEN;
-        PreRegs pf;
-        pf.v0 = prow[lane_id()];
-        pf.v1 = prow[64 + lane_id()];
-        if (bcast(pf.v1, PRE_STANCE - 64) != 0.0 && (!a.modes || qp_mask(a, rb, row) == 15)) {
-            solve_stance(a, rb, reinterpret_cast<const Prob*>(a.work + (size_t)row * WORK_LEN), pf,
-                         reinterpret_cast<const Presolve*>(prow), L.st);
-            return;
-        }
-    }
     solve_general_qp(a, rb, L);
 }
 
@@ -3577,7 +3445,7 @@ WBC_KERNEL_ATTR void wbc_solve_kernel(KernelArgs a) {
 // rare path; wbc_solve_kernel is the straight-line one.
 WBC_KERNEL_ATTR void wbc_solve_fallback_kernel(KernelArgs a) {
     __shared__ SolveLds L;
-    const int n = a.fb[a.parity];
+    const int n = min(a.fb[a.parity], a.fb_cap);
     for (int w = blockIdx.x; w < n; w += gridDim.x) {
         const int rb = a.fb[2 + w];
         wsync();
@@ -3599,7 +3467,7 @@ __device__ void solve_general_qp(const KernelArgs& a, int rb, SolveLds& L) {
                                reinterpret_cast<const double2*>(a.work + (size_t)row * WORK_LEN), lane_id());
     // the stance kernel's QP: checked after the problem copy is issued, so that a general QP's
     // loads all go out together (one HBM round trip)
-    if (WBC_STANCE_KERNEL && WBC_STANCE_ELIM && a.elim && kap_qp == 15 && bcast(pf.v1, PRE_STANCE - 64) != 0.0) return;
+    if (a.elim && kap_qp == 15 && bcast(pf.v1, PRE_STANCE - 64) != 0.0) return;
     if (a.modes) {  // this hypothesis' contact mask on the unmasked bounds (update_phase)
         const int kap = a.mode_masks[rb - row * a.modes] & 15;
         const int lane = lane_id();
@@ -3618,9 +3486,6 @@ __device__ void solve_general_qp(const KernelArgs& a, int rb, SolveLds& L) {
 // solved here, in the 12-variable force space; wbc_solve_kernel skips them.  A kernel of its own
 // so that its register and LDS budgets (no 24-variable state, no LDS copy of the problem) allow
 // WBC_STANCE_WAVES waves per SIMD instead of the general solve's 2.
-#ifndef WBC_AB_NO_FALLBACK
-#define WBC_AB_NO_FALLBACK 0
-#endif
 #ifndef WBC_STANCE_WAVES
 #define WBC_STANCE_WAVES 3  // 2 and 3 time the same; 4 spills (profiles/r02/d)
 #endif
@@ -3641,13 +3506,6 @@ void wbc_solve_stance_kernel(KernelArgs a) {
                  reinterpret_cast<const Presolve*>(prow), S);
 }
 
-#ifndef WBC_AB_FB_EMPTY
-#define WBC_AB_FB_EMPTY 0
-#endif
-__global__ void wbc_empty_kernel(int32_t* fb, int parity) {
-    if (fb[parity] < 0) fb[2] = 0;  // never true; keeps the load
-}
-
 __global__ void wbc_reset_kernel(double* hist, const uint8_t* mask, int batch) {
     const int rb = xcd_robot();
     if (rb >= batch) return;
@@ -3663,8 +3521,8 @@ extern "C" hipError_t wbc_launch_step(const wbc::KernelArgs* a, hipStream_t st) 
     hipLaunchKernelGGL(wbc::wbc_step_kernel, dim3(a->batch), dim3(64), 0, st, *a);
     return hipGetLastError();
 }
-extern "C" int wbc_kernel_default_split() { return WBC_DEFAULT_SPLIT; }
-extern "C" int wbc_kernel_stance_elim() { return WBC_STANCE_ELIM; }
+extern "C" int wbc_kernel_default_split() { return 1; }  // wbc_step: split kernels unless WBC_FUSED
+extern "C" int wbc_kernel_stance_elim() { return 1; }
 extern "C" hipError_t wbc_launch_update(const wbc::KernelArgs* a, hipStream_t st) {
     hipLaunchKernelGGL(wbc::wbc_update_kernel, dim3((a->batch + wbc::UPD_RPW - 1) / wbc::UPD_RPW), dim3(64), 0, st, *a);
     return hipGetLastError();
@@ -3676,24 +3534,17 @@ extern "C" hipError_t wbc_launch_solve_general(const wbc::KernelArgs* a, hipStre
     return hipGetLastError();
 }
 extern "C" hipError_t wbc_launch_solve_stance(const wbc::KernelArgs* a, hipStream_t st) {
-    if (!WBC_STANCE_ELIM) return hipSuccess;
-    if (!WBC_STANCE_KERNEL) return wbc_launch_solve_general(a, st);
     hipLaunchKernelGGL(wbc::wbc_solve_stance_kernel, dim3(a->batch), dim3(64), 0, st, *a);
-    if (!WBC_AB_NO_FALLBACK)  // A/B measurement builds only (-DWBC_AB_NO_FALLBACK=1): not a correct solve
-        hipLaunchKernelGGL(wbc::wbc_solve_fallback_kernel, dim3(16), dim3(64), 0, st, *a);
+    hipLaunchKernelGGL(wbc::wbc_solve_fallback_kernel, dim3(16), dim3(64), 0, st, *a);
     return hipGetLastError();
 }
 // Stateless all-stance step in two launches: the update kernel solving the stance QPs inline,
 // then the fallback kernel for the QPs whose elimination failed.
 extern "C" hipError_t wbc_launch_update_solve(const wbc::KernelArgs* a, hipStream_t st) {
-    if (!WBC_STANCE_ELIM || !a->elim || a->stateful || a->modes) return hipErrorInvalidValue;
+    if (!a->elim || a->stateful || a->modes) return hipErrorInvalidValue;
     hipLaunchKernelGGL(wbc::wbc_update_solve_kernel, dim3((a->batch + wbc::UPD_RPW - 1) / wbc::UPD_RPW), dim3(64), 0,
                        st, *a);
-#if WBC_AB_FB_EMPTY  // A/B timing builds only: an empty kernel in the fallback's place (not a correct solve)
-    hipLaunchKernelGGL(wbc::wbc_empty_kernel, dim3(16), dim3(64), 0, st, a->fb, a->parity);
-#elif !WBC_AB_NO_FALLBACK
     hipLaunchKernelGGL(wbc::wbc_solve_fallback_kernel, dim3(16), dim3(64), 0, st, *a);
-#endif
     return hipGetLastError();
 }
 extern "C" hipError_t wbc_launch_reset(double* hist, const uint8_t* mask, int batch, hipStream_t st) {

@@ -96,12 +96,13 @@ struct KernelArgs {
     const uint8_t* mode_masks;  // [modes]: contact mask of hypothesis k
     // Four-contact stance elimination (Presolve::stance) for this step's mask-15 QPs: the engine
     // turns it on when every QP of the step has mask 15 (then the stance solve kernel runs
-    // instead of the general one).  Mask-15 QPs whose elimination fails (a near-singular leg)
-    // are listed for the fallback solve: fb[parity] counts them, fb[2 ..] lists them; the update
-    // kernel clears fb[parity ^ 1] for the next update.
+    // instead of the general one).  QPs whose elimination did not happen (a near-singular leg)
+    // are listed for the fallback solve: fb[parity] counts them, fb[2 ..] lists them (at most
+    // fb_cap entries); the update kernel clears fb[parity ^ 1] for the next elimination update.
     int32_t elim;
     int32_t parity;
     int32_t* fb;
+    int32_t fb_cap;
     // the parameters by value: read from the kernel-argument segment (scalar loads of memory the
     // compiler knows is constant), not through `params`, whose global loads it must repeat after
     // every global store and wait for in turn

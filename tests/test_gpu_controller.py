@@ -57,3 +57,16 @@ def test_controller_stance_harness():
     assert res["cycles"] == 1000 and res["qp_status"] == 0
     # holding still under gravity: the knees carry the load
     assert np.all(np.isfinite(res["tau"])) and max(abs(t) for t in res["tau"]) < 80.0
+
+
+def test_controller_run_spins_callbacks_beside_the_control_thread():
+    """run() (hpp:41, cpp:678-683): the control loop on its own thread while the calling thread
+    spins the callbacks; a loop hook shuts the node down after 300 cycles.  With the stance
+    messages held fixed the controller settles to the stance harness's torques."""
+    r = subprocess.run([BIN, "run", "300"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["cycles"] == 300 and res["qp_status"] == 0 and res["messages"] > 0
+    s = subprocess.run([BIN, "stance", "300"], capture_output=True, text=True, timeout=300)
+    ref = json.loads(s.stdout.strip().splitlines()[-1])
+    assert close_to(res["tau"], ref["tau"], 1e-9), (res["tau"], ref["tau"])

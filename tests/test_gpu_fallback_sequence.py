@@ -1,0 +1,58 @@
+"""GPU: one engine stepped through alternating all-stance and mixed-mask steps, with and without
+elimination fallbacks (near-singular legs), every step checked against the C oracle.
+
+The fallback list of the stance elimination is a device counter per parity: an
+elimination update fills fb[p] and clears fb[p ^ 1] for the next elimination update.  The parity
+must therefore advance on elimination updates only; a mixed step in between (no elimination, no
+list) must neither advance it nor leave a stale list behind, or the third all-stance step of the
+sequence below re-solves the first step's failed robots from stale problem records over their
+fresh torques (and the count grows past the list's length).  Reference semantics: every cycle is
+solved from its own inputs (src/whole_body_controller.cpp:650-652).
+"""
+import numpy as np
+import pytest
+
+import wbc_ref as R
+from quadrupedwholebodycontroller_amd import STATELESS, Engine, workloads
+
+pytestmark = pytest.mark.gpu
+
+
+def close(a, b, tol):
+    return np.max(np.abs(a - b)) <= tol * (1.0 + np.max(np.abs(b)))
+
+
+def _steps(B):
+    st = workloads.stance_cold(B, seed=81)
+    straight = {k: v.copy() for k, v in st.items()}
+    for b in range(0, B, 5):  # a straight knee on one leg of every fifth robot: elimination fails
+        straight["qj"][b, 3 * (b % 4) + 2] = 0.0
+    mixed1 = workloads.rl_random(B, seed=82)
+    bent = workloads.stance_cold(B, seed=83)
+    mixed2 = workloads.rl_random(B, seed=84)
+    last = workloads.stance_cold(B, seed=85)
+    return [("stance_straight", straight), ("mixed", mixed1), ("stance_bent", bent), ("mixed", mixed2),
+            ("stance", last)]
+
+
+@pytest.mark.parametrize("split", [False, True])
+def test_alternating_stance_and_mixed_steps_match_oracle(split):
+    B = 200
+    e = Engine(B)
+    for t, (name, inp) in enumerate(_steps(B)):
+        e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
+        e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
+        if split:
+            e.update(STATELESS)
+            e.solve(STATELESS)
+        else:
+            e.step(STATELESS)
+        g = e.outputs()
+        o = R.run_batch(inp)
+        assert np.array_equal(g["status"], o["status"]), (t, name)
+        ok = o["status"] == 0
+        assert ok.sum() >= B // 2, (t, name)
+        for b in np.nonzero(ok)[0]:
+            assert close(g["tau"][b], o["tau"][b], 1e-7), (t, name, b)
+            assert close(g["grf"][b], o["grf"][b], 1e-7), (t, name, b)
+    e.close()
