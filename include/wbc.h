@@ -97,7 +97,7 @@ enum {
 /* Per-robot QP status (status[] output); 0 mirrors qpOASES SUCCESSFUL_RETURN (cpp:654). */
 enum {
     WBC_QP_OK = 0,
-    WBC_QP_MAX_ITER = 1,   /* more than max_wsr working-set changes (nWSR exceeded) */
+    WBC_QP_MAX_ITER = 1,   /* more than max_wsr working-set changes (nWSR exceeded; see iters below) */
     WBC_QP_INFEASIBLE = 2, /* constraints inconsistent */
     WBC_QP_NUMERIC = 3     /* non-finite input or factorisation breakdown */
 };
@@ -109,10 +109,11 @@ enum {
                           * SQProblem::hotstart, src/whole_body_controller.cpp:531). */
 #define WBC_DEBUG 2u     /* also write the per-robot debug record (wbc_get_debug) */
 #define WBC_NO_X 4u      /* skip the x[42] output (tau, grf, status, iters are still written) */
-#define WBC_SPLIT 8u     /* wbc_step as the update kernel + solve kernel pair instead of one fused kernel */
+#define WBC_SPLIT 8u     /* wbc_step / wbc_step_modes as the split kernels (update, then the general
+                          * 24-variable or four-contact solve kernel: wbc_update + wbc_solve) */
 #define WBC_TIMED 16u    /* wbc_step records HIP events around its kernels (wbc_last_kernel_ms) */
 #define WBC_COLD 32u     /* stateful, but the QP starts cold (no hotstart from the previous working set) */
-#define WBC_FUSED 64u    /* wbc_step as the single fused kernel (the build's default form may be the pair) */
+#define WBC_FUSED 64u    /* wbc_step as the one-robot-per-wave kernel of the general 24-variable method */
 
 /* Debug record layout (doubles per robot), written by update/step under WBC_DEBUG. */
 enum {
@@ -180,18 +181,28 @@ int32_t wbc_reset(wbc_engine* h, const uint8_t* mask);
 int32_t wbc_update(wbc_engine* h, uint32_t flags);
 /* solveQP() + computeJointTorques() on the problem assembled by the last wbc_update. */
 int32_t wbc_solve(wbc_engine* h, uint32_t flags);
-/* update + solve + torques for one control cycle: by default the update kernel then the solve
- * kernel (the problem passes through HBM; WBC_SPLIT forces this form), or under WBC_FUSED one fused
- * kernel (the problem stays in LDS). */
+/* update + solve + torques for one control cycle.  By default one kernel, four robots per wave:
+ * each robot's QP is reduced exactly to 12 variables (the swing slacks and stance equalities
+ * eliminated) and solved in place, any contact mask, stateless or stateful (with
+ * the hotstart); a robot whose reduction is not usable (a near-singular stance leg) is solved by
+ * the general method in a second launch.  WBC_SPLIT: the update kernel then the solve kernels,
+ * the problem passing through HBM (the form wbc_update + wbc_solve run); WBC_FUSED: one robot per
+ * wave, the general method with the problem in LDS.  All forms return the same x, tau and status;
+ * `iters` counts the working-set changes of the method that ran: the 12-variable form's friction
+ * and torque rows by default, the general form's rows (the swing slack rows included, the
+ * convention of a dense active set on the reference's 42 x 70 QP) under WBC_SPLIT / WBC_FUSED. */
 int32_t wbc_step(wbc_engine* h, uint32_t flags);
 int32_t wbc_synchronize(wbc_engine* h);
 
 /* Contact-mode hypotheses (BASELINE configs[4]: every state solved under several contact masks).
  * After wbc_set_modes(h, K, modes) with K dividing the batch B, the engine holds S = B / K states:
  * wbc_set_state / wbc_set_reference / bound device inputs hold S rows (contacts[] is not read), and
- * wbc_step_modes computes the dynamics and assembly (updateState, cpp:256-294) once per state, then
- * solves K QPs per state: output row s * K + k is state s under contact mask modes[k] (4-bit,
- * footContacts_ order), bit-identical to a wbc_step on that state with contacts = modes[k].
+ * wbc_step_modes solves K QPs per state: output row s * K + k is state s under contact mask
+ * modes[k] (4-bit, footContacts_ order), bit-identical to a wbc_step on that state with
+ * contacts = modes[k] (same flags).  By default each hypothesis runs in its own 16-lane segment
+ * (the state's inputs read from L2 by its K segments, nothing through HBM); WBC_SPLIT computes the
+ * dynamics and assembly (updateState, cpp:256-294) once per state and writes them to HBM for K
+ * general solves.
  * Hypotheses are cold steps: flags must include WBC_STATELESS (WBC_DEBUG is refused).
  * wbc_update / wbc_solve / wbc_step return WBC_ERR_STATE while modes are set; K = 0 clears them. */
 #define WBC_MAX_MODES 16

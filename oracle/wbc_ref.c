@@ -289,9 +289,11 @@ void wbc_ref_kindyn(const wbc_model* md, const double* pose, const double* nu, c
  * from the equality-constrained point, as a cold solve.  Re-adds are not counted in iters (only
  * working-set changes of the loop are).  On return act_out[0..*nact_out) holds the active
  * inequality ids (for the next hotstart). */
+/* selnorm / tolv (may be NULL): the selection scale of each inequality (slack / selnorm; default
+ * its row norm) and its violation tolerance (default 1e-10 max(1, |ci|)). */
 static int gi_solve(int n, const double* H, const double* g, int me, const double* CE, const double* ce, int mi,
                     const double* CI, const double* ci, int max_iter, const int* warm, int nwarm, double* x,
-                    int* iters_out, int* act_out, int* nact_out) {
+                    int* iters_out, int* act_out, int* nact_out, const double* selnorm, const double* tolv) {
     double L[NV * NV], J[NV * NV], R[NV * NV], u[NV], d[NV], z[NV], r[NV], ni[2 * NC], x0[NV];
     if (nact_out) *nact_out = 0;
     int act[NV]; /* >= 0: inequality id ; < 0: equality -(id+1) */
@@ -340,6 +342,7 @@ static int gi_solve(int n, const double* H, const double* g, int me, const doubl
     for (int i = 0; i < mi; ++i) {
         double s = 0.0;
         for (int k = 0; k < n; ++k) s += CI[i * n + k] * CI[i * n + k];
+        if (selnorm) s = selnorm[i] * selnorm[i];
         ni[i] = sqrt(s > 1e-300 ? s : 1e-300);
     }
 #define COMPUTE_DZR(np_)                                                               \
@@ -487,7 +490,7 @@ static int gi_solve(int n, const double* H, const double* g, int me, const doubl
             if (isact) continue;
             double s = -ci[i];
             for (int k = 0; k < n; ++k) s += CI[i * n + k] * x[k];
-            double tol = 1e-10 * (fabs(ci[i]) > 1.0 ? fabs(ci[i]) : 1.0);
+            double tol = tolv ? tolv[i] : 1e-10 * (fabs(ci[i]) > 1.0 ? fabs(ci[i]) : 1.0);
             if (s < -tol && s / ni[i] < best) { best = s / ni[i]; p = i; }
         }
         if (p < 0) { *iters_out = iters; GI_RETURN(WBC_REF_OK); }
@@ -586,13 +589,287 @@ static int solve_qp(const double* H, const double* g, const double* A, const dou
             ci[mi++] = -ub[i];
         }
     }
-    return gi_solve(n, H, g, me, CE, ce, mi, CI, ci, max_iter, warm, nwarm, x, iters, act_out, nact_out);
+    return gi_solve(n, H, g, me, CE, ce, mi, CI, ci, max_iter, warm, nwarm, x, iters, act_out, nact_out, NULL, NULL);
 }
 
 /* The dense Goldfarb-Idnani above for other callers (oracle/wbc_fast.c), cold (no warm set). */
 int wbc_ref_gi(int n, const double* H, const double* g, int me, const double* CE, const double* ce, int mi, const double* CI,
                const double* ci, int max_iter, double* x, int* iters) {
-    return gi_solve(n, H, g, me, CE, ce, mi, CI, ci, max_iter, NULL, 0, x, iters, NULL, NULL);
+    return gi_solve(n, H, g, me, CE, ce, mi, CI, ci, max_iter, NULL, 0, x, iters, NULL, NULL, NULL, NULL);
+}
+
+/* ------------------------------------------------------------------ the engine's 12-variable form */
+/* The same QP reduced exactly to 12 variables for every contact mask (the numpy
+ * restatement oracle/wbc_reduced.py documents the derivation): z = one 3-slot per leg (a swing
+ * leg's joint accelerations, a stance leg's force); a and the swing slacks eliminated (s_i = |r_i|,
+ * the pair of slack rows becomes the penalty 1/2 w r_i^2), the stance equalities solved for the
+ * stance joints by Woodbury (qdd_S = q0 + Y phi, phi = B z).  Inequality rows in the engine's
+ * numbering: friction face 4 l + rr of stance leg l, torque row 16 + 2 j (+ side) / 16 + 2 j + 1
+ * (- side).  Selected by slack / |reference row| with the reference row's tolerance, as the
+ * kernel (wbc_kernel.hip solve16) does, so both count the same working-set changes; hotstart from
+ * the previous solve's set in this numbering (friction rows of legs no longer in contact dropped).
+ * Returns the QP status, or -1 when the elimination is not usable (a near-singular stance leg or
+ * S6): the engine then solves the literal form, and so does the caller. */
+static int reduced_solve(const wbc_params* pr, wbc_ref_state* st, const wbc_ref_kindyn_t* kd, const double* T,
+                         const double* Tinv, const double* Mbar_b, const double* Mbar_j, const double* bbar,
+                         const double* W, const double* r1, const double* rsw, const int* kap, double* x, double* tau,
+                         int* iters) {
+    double Jbar[12 * ND], E[12 * 6], Jbj[144], K[6 * 12], Jl[4][9];
+    mat_mul(kd->foot_J, Tinv, Jbar, 12, ND, ND);
+    for (int i = 0; i < 12; ++i) {
+        for (int c = 0; c < 6; ++c) E[i * 6 + c] = Jbar[i * ND + c];
+        for (int j = 0; j < 12; ++j) Jbj[i * 12 + j] = Jbar[i * ND + 6 + j];
+    }
+    for (int a = 0; a < 6; ++a)
+        for (int j = 0; j < 12; ++j) K[a * 12 + j] = T[a * ND + 6 + j]; /* Jbj = Jblk - E K */
+    for (int l = 0; l < 4; ++l)
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) Jl[l][3 * r + c] = kd->foot_J[(3 * l + r) * ND + 6 + 3 * l + c];
+    double Mbi[36];
+    if (mat_inv(Mbar_b, Mbi, 6)) return -1;
+    const double g0 = pr->gravity, wsw = pr->slack_weight;
+    int stj[12];
+    for (int i = 0; i < 12; ++i) stj[i] = kap[i / 3];
+    /* stance rows: W = J_S^-1 E_S, w = J_S^-1 e_S */
+    double Wr[72] = {0}, w[12] = {0};
+    for (int l = 0; l < 4; ++l) {
+        if (!kap[l]) continue;
+        double Ji[9], det, amx = 0.0;
+        for (int t = 0; t < 9; ++t) amx = fmax(amx, fabs(Jl[l][t]));
+        double c00 = Jl[l][4] * Jl[l][8] - Jl[l][5] * Jl[l][7], c01 = Jl[l][5] * Jl[l][6] - Jl[l][3] * Jl[l][8],
+               c02 = Jl[l][3] * Jl[l][7] - Jl[l][4] * Jl[l][6];
+        det = Jl[l][0] * c00 + Jl[l][1] * c01 + Jl[l][2] * c02;
+        if (!(fabs(det) > 1e-9 * amx * amx * amx)) return -1;
+        if (mat_inv(Jl[l], Ji, 3)) return -1;
+        for (int k = 0; k < 3; ++k) {
+            const int i = 3 * l + k;
+            for (int c = 0; c < 6; ++c) {
+                double t = 0.0;
+                for (int kk = 0; kk < 3; ++kk) t += Ji[k * 3 + kk] * E[(3 * l + kk) * 6 + c];
+                Wr[i * 6 + c] = t;
+            }
+            double t = 0.0;
+            for (int kk = 0; kk < 3; ++kk) t += Ji[k * 3 + kk] * (r1[3 * l + kk] + (kk == 2 ? g0 : 0.0));
+            w[i] = t;
+        }
+    }
+    double S6[36], S6i[36], z6[6];
+    for (int a = 0; a < 6; ++a) {
+        for (int b = 0; b < 6; ++b) {
+            double t = (a == b) ? 1.0 : 0.0;
+            for (int j = 0; j < 12; ++j) t -= K[a * 12 + j] * Wr[j * 6 + b];
+            S6[a * 6 + b] = t;
+        }
+        double t = 0.0;
+        for (int j = 0; j < 12; ++j) t += K[a * 12 + j] * w[j];
+        z6[a] = t;
+    }
+    {
+        double smx = 0.0, pmin = 1e300, LU[36];
+        for (int t = 0; t < 36; ++t) smx = fmax(smx, fabs(S6[t]));
+        memcpy(LU, S6, sizeof LU); /* pivots of Gauss-Jordan without pivoting, as the kernel */
+        for (int k = 0; k < 6; ++k) {
+            pmin = fmin(pmin, fabs(LU[k * 6 + k]));
+            for (int i = k + 1; i < 6; ++i) {
+                const double f = LU[i * 6 + k] / LU[k * 6 + k];
+                for (int j = k; j < 6; ++j) LU[i * 6 + j] -= f * LU[k * 6 + j];
+            }
+        }
+        if (!(pmin > 1e-6 * smx)) return -1;
+        if (mat_inv(S6, S6i, 6)) return -1;
+    }
+    double Y[72], q0[12];
+    for (int i = 0; i < 12; ++i) {
+        double q = w[i];
+        for (int c = 0; c < 6; ++c) {
+            double t = 0.0;
+            for (int b = 0; b < 6; ++b) t += Wr[i * 6 + b] * S6i[b * 6 + c];
+            Y[i * 6 + c] = t;
+            q += t * z6[c];
+        }
+        q0[i] = q;
+    }
+    /* B (phi = B z), P (E_S^T f), the leg rows Rho = own + v^T B with rho0 and weights */
+    double B[6 * 12] = {0}, P[6 * 12] = {0}, cpsi[6] = {0, 0, -g0, 0, 0, 0};
+    for (int j = 0; j < 12; ++j) {
+        for (int a = 0; a < 6; ++a) {
+            if (stj[j]) {
+                double t = 0.0;
+                for (int b = 0; b < 6; ++b) t += Mbi[a * 6 + b] * E[j * 6 + b];
+                B[a * 12 + j] = -t;
+                P[a * 12 + j] = E[j * 6 + a];
+            } else {
+                B[a * 12 + j] = K[a * 12 + j];
+            }
+            if (stj[j]) cpsi[a] -= K[a * 12 + j] * q0[j];
+        }
+    }
+    double Rho[144] = {0}, rho0[12], wt[12], V6[72];
+    for (int i = 0; i < 12; ++i) {
+        const int l = i / 3, k = i % 3;
+        double v[6];
+        if (stj[i]) {
+            for (int c = 0; c < 6; ++c) v[c] = Y[i * 6 + c];
+            rho0[i] = q0[i];
+            wt[i] = 1.0;
+        } else {
+            for (int c = 0; c < 6; ++c) {
+                double t = 0.0;
+                for (int b = 0; b < 6; ++b) t += S6i[b * 6 + c] * E[i * 6 + b];
+                v[c] = -t;
+            }
+            double ec = 0.0;
+            for (int c = 0; c < 6; ++c) ec += E[i * 6 + c] * cpsi[c];
+            rho0[i] = ec - rsw[i];
+            wt[i] = wsw;
+            for (int c = 0; c < 3; ++c) Rho[i * 12 + 3 * l + c] = Jl[l][3 * k + c];
+        }
+        for (int c = 0; c < 6; ++c) V6[i * 6 + c] = v[c];
+        for (int j = 0; j < 12; ++j) {
+            double t = 0.0;
+            for (int c = 0; c < 6; ++c) t += v[c] * B[c * 12 + j];
+            Rho[i * 12 + j] += t;
+        }
+    }
+    double H[144], g[12];
+    {
+        double CP[36];
+        for (int a = 0; a < 6; ++a)
+            for (int b = 0; b < 6; ++b) {
+                double t = (a == b) ? 1.0 : 0.0;
+                for (int c = 0; c < 6; ++c) t += Mbi[a * 6 + c] * Mbi[c * 6 + b];
+                CP[a * 6 + b] = t;
+            }
+        for (int a = 0; a < 12; ++a)
+            for (int j = 0; j < 12; ++j) {
+                double t = (a == j) ? 1.0 : 0.0;
+                for (int c = 0; c < 6; ++c)
+                    for (int d = 0; d < 6; ++d) t += P[c * 12 + a] * CP[c * 6 + d] * P[d * 12 + j];
+                for (int i = 0; i < 12; ++i) t += wt[i] * Rho[i * 12 + a] * Rho[i * 12 + j];
+                H[a * 12 + j] = t;
+            }
+        const double wv[6] = {W[0], W[1], W[2] + g0 / (Mbar_b[0]), W[3], W[4], W[5]};
+        for (int a = 0; a < 12; ++a) {
+            double t = 0.0;
+            for (int c = 0; c < 6; ++c) t -= P[c * 12 + a] * wv[c];
+            for (int i = 0; i < 12; ++i) t += wt[i] * Rho[i * 12 + a] * rho0[i];
+            g[a] = t;
+        }
+    }
+    /* torque map and the inequality rows */
+    double t0[12], Nt[144], nselr[12];
+    for (int r = 0; r < 12; ++r) {
+        double my[6] = {0}, t = bbar[6 + r], s2 = 0.0;
+        for (int s_ = 0; s_ < 12; ++s_) {
+            const double mk = Mbar_j[r * 12 + s_];
+            s2 += mk * mk;
+            if (stj[s_]) {
+                s2 += Jbj[s_ * 12 + r] * Jbj[s_ * 12 + r];
+                t += mk * q0[s_];
+                for (int c = 0; c < 6; ++c) my[c] += mk * Y[s_ * 6 + c];
+            }
+        }
+        t0[r] = t;
+        nselr[r] = s2;
+        for (int j = 0; j < 12; ++j) {
+            double v = stj[j] ? Jbj[j * 12 + r] : -Mbar_j[r * 12 + j];
+            for (int c = 0; c < 6; ++c) v -= my[c] * B[c * 12 + j];
+            Nt[r * 12 + j] = v;
+        }
+    }
+    const double mu = pr->friction, tm = pr->max_torque;
+    const double D[12] = {1, 0, -mu, -1, 0, -mu, 0, 1, -mu, 0, -1, -mu};
+    double CI[40 * 12], ci[40], seln[40], tolv[40];
+    int ids[40], mi = 0, idpos[40];
+    for (int t = 0; t < 40; ++t) idpos[t] = -1;
+    for (int l = 0; l < 4; ++l) {
+        if (!kap[l]) continue;
+        for (int rr = 0; rr < 4; ++rr) {
+            for (int j = 0; j < 12; ++j) CI[mi * 12 + j] = 0.0;
+            for (int c = 0; c < 3; ++c) CI[mi * 12 + 3 * l + c] = -D[rr * 3 + c];
+            ci[mi] = 0.0;
+            seln[mi] = sqrt(1.0 + mu * mu);
+            tolv[mi] = 1e-10;
+            ids[mi] = 4 * l + rr;
+            idpos[4 * l + rr] = mi;
+            ++mi;
+        }
+    }
+    for (int j = 0; j < 12; ++j)
+        for (int side = 0; side < 2; ++side) {
+            const double sg = side ? -1.0 : 1.0;
+            for (int c = 0; c < 12; ++c) CI[mi * 12 + c] = -sg * Nt[j * 12 + c];
+            ci[mi] = -tm - sg * t0[j];
+            seln[mi] = sqrt(nselr[j] > 1e-300 ? nselr[j] : 1e-300);
+            const double bref = -tm - sg * bbar[6 + j];
+            tolv[mi] = 1e-10 * (fabs(bref) > 1.0 ? fabs(bref) : 1.0);
+            ids[mi] = 16 + 2 * j + side;
+            idpos[16 + 2 * j + side] = mi;
+            ++mi;
+        }
+    /* vacuous rows (quirk A.12): a swing leg's R1 row reads 0 = r1 */
+    for (int i = 0; i < 12; ++i)
+        if (!stj[i] && fabs(r1[i]) > 1e-9 * (fabs(r1[i]) > 1.0 ? fabs(r1[i]) : 1.0)) {
+            *iters = 0;
+            st->ws12 = 0;
+            st->ws12_valid = 1;
+            return WBC_REF_INFEASIBLE;
+        }
+    int warm[12], nwarm = 0;
+    if (st->first && !st->cold_qp && st->ws12_valid) {
+        for (int id = 0; id < 40; ++id)
+            if (((st->ws12 >> id) & 1ull) && idpos[id] >= 0) {
+                if (nwarm < 12) warm[nwarm] = idpos[id];
+                ++nwarm;
+            }
+        if (nwarm > 12) nwarm = 0;
+    }
+    double z[NV]; /* gi_solve saves and restores NV entries (warm start) */
+    int act[NV], nact = 0;
+    const int status = gi_solve(12, H, g, 0, NULL, NULL, mi, CI, ci, pr->max_wsr, nwarm ? warm : NULL, nwarm, z, iters, act,
+                                &nact, seln, tolv);
+    st->ws12 = 0;
+    st->ws12_valid = 1;
+    if (status == WBC_REF_OK)
+        for (int k = 0; k < nact; ++k) st->ws12 |= 1ull << ids[act[k]];
+    if (status != WBC_REF_OK) return status;
+    /* back to the 42 variables */
+    double phi[6];
+    for (int c = 0; c < 6; ++c) {
+        double t = 0.0;
+        for (int j = 0; j < 12; ++j) t += B[c * 12 + j] * z[j];
+        phi[c] = t;
+    }
+    double ef[6];
+    for (int c = 0; c < 6; ++c) {
+        double t = 0.0;
+        for (int j = 0; j < 12; ++j) t += P[c * 12 + j] * z[j];
+        ef[c] = t;
+    }
+    for (int a = 0; a < 6; ++a) {
+        double t = (a == 2) ? -g0 : 0.0;
+        for (int b = 0; b < 6; ++b) t += Mbi[a * 6 + b] * ef[b];
+        x[a] = t;
+    }
+    for (int i = 0; i < 12; ++i) {
+        double qv = z[i];
+        if (stj[i]) {
+            qv = q0[i];
+            for (int c = 0; c < 6; ++c) qv += Y[i * 6 + c] * phi[c];
+        }
+        x[6 + i] = qv;
+        x[18 + i] = stj[i] ? z[i] : 0.0;
+        double r = rho0[i];
+        for (int j = 0; j < 12; ++j) r += Rho[i * 12 + j] * z[j];
+        x[30 + i] = stj[i] ? fabs(rsw[i]) : fabs(r);
+    }
+    for (int r = 0; r < 12; ++r) {
+        double t = t0[r];
+        for (int j = 0; j < 12; ++j) t -= Nt[r * 12 + j] * z[j];
+        tau[r] = t;
+    }
+    (void)V6;
+    return status;
 }
 
 /* ------------------------------------------------------------------ controller */
@@ -774,11 +1051,36 @@ int wbc_ref_step(const wbc_model* md, const wbc_params* pr, wbc_ref_state* st, c
         }
     }
     int it = 0, nact = 0, act[NV];
+    int status = -1;
+    if (st->method == 1) {
+        /* the engine's 12-variable form; -1: not usable here, the literal form below */
+        double Tinv_r[ND * ND], rsw[12];
+        for (int i = 0; i < 12; ++i) rsw[i] = ub[46 + i];
+        if (mat_inv(T, Tinv_r, ND) == 0)
+            status = reduced_solve(pr, st, &kd, T, Tinv_r, Mbar_b, Mbar_j, bbar, W, lb + 6, rsw, kap, x, tau, &it);
+        if (status < 0) st->ws12_valid = 0;
+        else {
+            *iters = it;
+            st->contacts = contacts;
+            st->first = 1;
+            st->ws_n = 0;
+            if (status != WBC_REF_OK) {
+                memset(x, 0, sizeof(double) * NV);
+                memset(tau, 0, sizeof(double) * NJ);
+                memset(grf, 0, sizeof(double) * NJ);
+            } else {
+                for (int i = 0; i < NJ; ++i) grf[i] = x[18 + i];
+            }
+            goto debug_out;
+        }
+    }
     /* init on the first cycle, hotstart from the previous working set afterwards (cpp:523-531);
      * the working set only carries over under the same contact mask (the constraint rows differ
      * otherwise) */
+    {
     const int warm = st->first && !st->cold_qp && st->ws_n > 0 && st->ws_kap == contacts;
-    int status = solve_qp(H, g, A, lb, ub, pr->max_wsr, warm ? st->ws : NULL, warm ? st->ws_n : 0, x, &it, act, &nact);
+    status = solve_qp(H, g, A, lb, ub, pr->max_wsr, warm ? st->ws : NULL, warm ? st->ws_n : 0, x, &it, act, &nact);
+    }
     *iters = it;
     st->contacts = contacts;
     st->first = 1;
@@ -799,6 +1101,7 @@ int wbc_ref_step(const wbc_model* md, const wbc_params* pr, wbc_ref_state* st, c
             grf[i] = x[18 + i];
         }
     }
+debug_out:
     if (dbg) {
         memcpy(dbg->com, kd.com, sizeof kd.com);
         memcpy(dbg->comvel, kd.com_vel, sizeof kd.com_vel);
@@ -818,9 +1121,16 @@ int wbc_ref_step(const wbc_model* md, const wbc_params* pr, wbc_ref_state* st, c
 void wbc_ref_run_batch(const wbc_model* md, const wbc_params* pr, int B, const double* pose, const double* nu,
                        const double* qj, const double* ref, const uint8_t* contacts, const uint8_t* switching, double* tau,
                        double* grf, double* x, int32_t* status, int32_t* iters) {
+    wbc_ref_run_batch_method(md, pr, B, pose, nu, qj, ref, contacts, switching, tau, grf, x, status, iters, 0);
+}
+
+void wbc_ref_run_batch_method(const wbc_model* md, const wbc_params* pr, int B, const double* pose, const double* nu,
+                              const double* qj, const double* ref, const uint8_t* contacts, const uint8_t* switching,
+                              double* tau, double* grf, double* x, int32_t* status, int32_t* iters, int method) {
     for (int b = 0; b < B; ++b) {
         wbc_ref_state st;
         wbc_ref_state_init(&st);
+        st.method = method;
         int it = 0;
         status[b] = wbc_ref_step(md, pr, &st, pose + 7 * b, nu + 18 * b, qj + 12 * b, ref + 54 * b, contacts[b],
                                  switching[b], tau + 12 * b, grf + 12 * b, x + NV * b, &it, NULL);

@@ -21,6 +21,10 @@ typedef struct {
     int contacts, first;
     int ws_n, ws_kap, cold_qp; /* working set of the last solve (hotstart, cpp:531); cold_qp: always init */
     int ws[42];
+    /* QP method: 0 = the literal 42 x 70 QP (dense Goldfarb-Idnani), 1 = the engine's exact
+     * 12-variable form of the same QP (its working set in ws12, row ids of that form) */
+    int method, ws12_valid;
+    unsigned long long ws12;
 } wbc_ref_state;
 
 typedef struct {
@@ -36,6 +40,10 @@ int wbc_ref_step(const wbc_model* md, const wbc_params* pr, wbc_ref_state* st, c
 void wbc_ref_run_batch(const wbc_model* md, const wbc_params* pr, int B, const double* pose, const double* nu,
                        const double* qj, const double* ref, const uint8_t* contacts, const uint8_t* switching, double* tau,
                        double* grf, double* x, int32_t* status, int32_t* iters);
+/* the same with QP method `method` (wbc_ref_state::method) */
+void wbc_ref_run_batch_method(const wbc_model* md, const wbc_params* pr, int B, const double* pose, const double* nu,
+                              const double* qj, const double* ref, const uint8_t* contacts, const uint8_t* switching,
+                              double* tau, double* grf, double* x, int32_t* status, int32_t* iters, int method);
 int wbc_ref_gi(int n, const double* H, const double* g, int me, const double* CE, const double* ce, int mi, const double* CI,
                const double* ci, int max_iter, double* x, int* iters);
 

@@ -29,7 +29,11 @@ class State(C.Structure):
     _fields_ = [("old_T", C.c_double * 324), ("old_Jc", C.c_double * 216), ("old_Js", C.c_double * 216),
                 ("Tdot_inv", C.c_double * 324), ("e_int", C.c_double * 6), ("contacts", C.c_int),
                 ("first", C.c_int), ("ws_n", C.c_int), ("ws_kap", C.c_int), ("cold_qp", C.c_int),
-                ("ws", C.c_int * 42)]
+                ("ws", C.c_int * 42), ("method", C.c_int), ("ws12_valid", C.c_int), ("ws12", C.c_ulonglong)]
+
+# QP methods of the restatement (wbc_ref_state::method): the literal 42 x 70 QP, and the engine's
+# exact 12-variable form of the same QP (its iteration convention: tests compare `iters` with it)
+LITERAL, REDUCED = 0, 1
 
 
 class Debug(C.Structure):
@@ -51,6 +55,7 @@ def lib():
         _lib.wbc_ref_step.argtypes = [P, P, P, P, P, P, P, C.c_int, C.c_int, P, P, P, P, P]
         _lib.wbc_ref_step.restype = C.c_int
         _lib.wbc_ref_run_batch.argtypes = [P, P, C.c_int, P, P, P, P, P, P, P, P, P, P, P]
+        _lib.wbc_ref_run_batch_method.argtypes = [P, P, C.c_int, P, P, P, P, P, P, P, P, P, P, P, C.c_int]
         _bind_baseline(_lib)
     return _lib
 
@@ -157,9 +162,10 @@ def _p(a):
     return a.ctypes.data_as(C.c_void_p)
 
 
-def run_batch(inp, **overrides):
+def run_batch(inp, method=LITERAL, **overrides):
     """Cold batch (every robot from setInitialState with the given switching flags).  Keyword
-    arguments override wbc_params fields (e.g. max_torque=6.0, max_wsr=2)."""
+    arguments override wbc_params fields (e.g. max_torque=6.0, max_wsr=2).  method: LITERAL (the
+    42 x 70 QP as assembled at cpp:466-515) or REDUCED (the engine's 12-variable form)."""
     m, p = model_params()
     if overrides:
         p2 = type(p)()
@@ -173,20 +179,23 @@ def run_batch(inp, **overrides):
     con, sw = f("contacts", np.uint8), f("switching", np.uint8)
     out = dict(tau=np.zeros((B, 12)), grf=np.zeros((B, 12)), x=np.zeros((B, 42)), status=np.zeros(B, np.int32),
                iters=np.zeros(B, np.int32))
-    lib().wbc_ref_run_batch(C.byref(m), C.byref(p), B, _p(pose), _p(nu), _p(qj), _p(ref), _p(con), _p(sw),
-                            _p(out["tau"]), _p(out["grf"]), _p(out["x"]), _p(out["status"]), _p(out["iters"]))
+    lib().wbc_ref_run_batch_method(C.byref(m), C.byref(p), B, _p(pose), _p(nu), _p(qj), _p(ref), _p(con), _p(sw),
+                                   _p(out["tau"]), _p(out["grf"]), _p(out["x"]), _p(out["status"]), _p(out["iters"]),
+                                   int(method))
     return out
 
 
 class Robot:
     """Stateful single robot (the reference object across cycles)."""
 
-    def __init__(self, hotstart=True, **overrides):
+    def __init__(self, hotstart=True, method=LITERAL, **overrides):
         """hotstart: qpOASES init on the first cycle, then hotstart from the previous working set
-        (cpp:523-531); False: every solve cold (the engine's WBC_COLD).  overrides: wbc_params fields."""
+        (cpp:523-531); False: every solve cold (the engine's WBC_COLD).  method: LITERAL or REDUCED
+        (the QP form, see run_batch).  overrides: wbc_params fields."""
         self.st = State()
         lib().wbc_ref_state_init(C.byref(self.st))
         self.st.cold_qp = 0 if hotstart else 1
+        self.st.method = int(method)
         self.overrides = overrides
 
     def step(self, pose, nu, qj, ref, contacts, switching, debug=False):

@@ -18,7 +18,6 @@ extern "C" hipError_t wbc_launch_update(const wbc::KernelArgs* a, hipStream_t st
 extern "C" hipError_t wbc_launch_solve_general(const wbc::KernelArgs* a, hipStream_t st);
 extern "C" hipError_t wbc_launch_solve_stance(const wbc::KernelArgs* a, hipStream_t st);
 extern "C" hipError_t wbc_launch_update_solve(const wbc::KernelArgs* a, hipStream_t st);
-extern "C" int wbc_kernel_default_split();
 extern "C" hipError_t wbc_launch_reset(double* hist, const uint8_t* mask, int batch, hipStream_t st);
 extern "C" int wbc_kernel_stance_elim();
 
@@ -187,6 +186,15 @@ void begin_update(wbc_engine* h, wbc::KernelArgs& a) {
     if (h->elim) h->parity ^= 1;
     a.elim = h->elim ? 1 : 0;
     a.parity = h->elim_parity;
+}
+
+// The default step (wbc_update_solve_kernel: every QP reduced to 12 variables and solved in the
+// update wave): it fills the fallback list of its parity like an elimination update
+void begin_step16(wbc_engine* h, wbc::KernelArgs& a) {
+    a.elim = 1;
+    a.parity = h->parity;
+    h->parity ^= 1;
+    h->elim = false;  // a later wbc_solve needs its own wbc_update
 }
 
 hipError_t launch_solves(wbc_engine* h, wbc::KernelArgs& a) {
@@ -453,19 +461,17 @@ int32_t wbc_step(wbc_engine* h, uint32_t flags) {
     wbc::KernelArgs a = make_args(h, flags);
     const bool timed = (flags & WBC_TIMED) != 0;  // event packets cost a few us between kernels
     if (timed) WBC_HIP(hipEventRecord(h->ev0, h->stream));
-    // default form chosen at build time (WBC_DEFAULT_SPLIT, by measurement); the flags force one
-    const bool split = (flags & WBC_SPLIT) || (!(flags & WBC_FUSED) && wbc_kernel_default_split());
-    if (split) {
+    if (flags & WBC_SPLIT) {
+        // the split kernels: update (records to HBM), then the general / stance solve kernels
         begin_update(h, a);
-        if (h->elim && !a.stateful) {
-            // stateless all-stance step: the update kernel solves the stance QPs itself
-            WBC_HIP(wbc_launch_update_solve(&a, h->stream));
-        } else {
-            WBC_HIP(wbc_launch_update(&a, h->stream));
-            WBC_HIP(launch_solves(h, a));
-        }
+        WBC_HIP(wbc_launch_update(&a, h->stream));
+        WBC_HIP(launch_solves(h, a));
+    } else if (flags & WBC_FUSED) {
+        WBC_HIP(wbc_launch_step(&a, h->stream));  // one robot per wave, the general method
     } else {
-        WBC_HIP(wbc_launch_step(&a, h->stream));
+        // default: one kernel, every QP reduced to 12 variables and solved in the update wave
+        begin_step16(h, a);
+        WBC_HIP(wbc_launch_update_solve(&a, h->stream));
     }
     if (timed) {
         WBC_HIP(hipEventRecord(h->ev1, h->stream));
@@ -502,13 +508,21 @@ int32_t wbc_step_modes(wbc_engine* h, uint32_t flags) {
     WBC_HIP(hipSetDevice(h->device));
     wbc::KernelArgs a = make_args(h, flags);
     a.modes = h->n_modes;
-    begin_update(h, a);
     const bool timed = (flags & WBC_TIMED) != 0;
     if (timed) WBC_HIP(hipEventRecord(h->ev0, h->stream));
-    wbc::KernelArgs au = a;  // the update runs once per state
-    au.batch = h->batch / h->n_modes;
-    WBC_HIP(wbc_launch_update(&au, h->stream));
-    WBC_HIP(launch_solves(h, a));
+    if (flags & WBC_SPLIT) {
+        // split form: the update once per state (problem records to HBM), the general / stance
+        // solve kernels once per hypothesis
+        begin_update(h, a);
+        wbc::KernelArgs au = a;
+        au.batch = h->batch / h->n_modes;
+        WBC_HIP(wbc_launch_update(&au, h->stream));
+        WBC_HIP(launch_solves(h, a));
+    } else {
+        // default: each hypothesis reduced and solved in its own 16-lane segment
+        begin_step16(h, a);
+        WBC_HIP(wbc_launch_update_solve(&a, h->stream));
+    }
     if (timed) {
         WBC_HIP(hipEventRecord(h->ev1, h->stream));
         h->timed = true;

@@ -81,25 +81,40 @@ struct UpdScratch {
     double yv[6];           // Tdot_inv nu exchange (segmented update kernel)
 };
 
-// The update kernel's inline stance solve (solve_stance16) works in the robot's own UpdScratch,
-// in arrays the update no longer reads once stance_reduce has formed Nt: the force-space factor
-// M and f0 stay where factor12 leaves them (ps.L, ps.xs), the rest goes here.
+// The update kernel's inline solve (solve16) works in the robot's own UpdScratch and Prob, in
+// arrays the update no longer reads once the reduction has formed the torque map: the factor
+// (J mirror) and x0 stay where the factorisation leaves them (ps.L, ps.xs), the rest goes here.
+// Two placements: the four-contact stance form (stance_reduce, stateless all-stance waves) and
+// the general form of every contact mask (reduce_general, §4.8), whose torque map overwrites the
+// problem's Jbar joint block and which keeps the maps back to the 42 variables for the outputs.
 struct St16 {
-    double* Nt;    // [12][12] torque map rows (ja .. A: 204 doubles)
-    double* Y;     // [12][6]  (in)
-    double* t0;    // [12]     (in + 72)
-    double* q0;    // [12]     (sc)
-    double* nsel;  // [12]     (sc + 12): |reference torque row|^2
+    double* Nt;    // [12][12] torque map rows: stance ja .. A (204 doubles); general P.Jbj
+    double* Y;     // [12][6]  stance in; general sr.Y
+    double* t0;    // [12]     stance in + 72; general pf
+    double* q0;    // [12]     stance sc; general sr.q0
+    double* nsel;  // [12]     sc + 12: |reference torque row|^2
     double* col;   // [16]     column exchange: d (12), slack, Givens pair (KA)
-    double* ucon;  // [48]     multiplier per constraint (Mjj, hj)
-    double* f;     // [12]     primal forces (cen)
+    double* f;     // [12]     primal (stance: cen; general: KA + 16)
+    // general form only
+    double* Bt;    // [12][6]  phi = B z: column j of B (ja, jo)
+    double* Vt;    // [12][6]  leg row i: its coupling v_i to phi (in)
+    double* rho0;  // [12]     leg row i at z = 0 (in + 72)
+    double* Ct;    // [12][6]  P_j (stance slot) or o_j (swing slot), Hessian assembly (Mjj, hj, cen)
+    double* J0;    // [12][12] copy of the initial J rows for a rejected hotstart (P.Mbj)
     __device__ explicit St16(UpdScratch& s)
         : Nt(&s.ja[0][0]), Y(&s.in[0]), t0(&s.in[72]), q0(&s.sc[0][0]), nsel(&s.sc[6][0]), col(&s.KA[0][0]),
-          ucon(&s.Mjj[0][0]), f(&s.cen[0]) {}
+          f(&s.cen[0]), Bt(nullptr), Vt(nullptr), rho0(nullptr), Ct(nullptr), J0(nullptr) {}
+    __device__ St16(UpdScratch& s, Prob& P)
+        : Nt(&P.Jbj[0]), Y(&s.sr.Y[0][0]), t0(&s.pf[0][0]), q0(&s.sr.q0[0]), nsel(&s.sc[6][0]), col(&s.KA[0][0]),
+          f(&s.KA[0][0] + 16), Bt(&s.ja[0][0]), Vt(&s.in[0]), rho0(&s.in[72]), Ct(&s.Mjj[0][0]), J0(&P.Mbj[0]) {}
 };
 static_assert(offsetof(UpdScratch, A) + sizeof(UpdScratch::A) - offsetof(UpdScratch, ja) >= 144 * sizeof(double), "St16 Nt");
-static_assert(offsetof(UpdScratch, hj) == offsetof(UpdScratch, Mjj) + sizeof(UpdScratch::Mjj), "St16 ucon");
-static_assert(sizeof(UpdScratch::hj) + sizeof(UpdScratch::Mjj) >= 48 * sizeof(double), "St16 ucon");
+static_assert(offsetof(UpdScratch, jo) == offsetof(UpdScratch, ja) + sizeof(UpdScratch::ja), "St16 Bt");
+static_assert(offsetof(UpdScratch, vf) == offsetof(UpdScratch, pf) + sizeof(UpdScratch::pf), "St16 t0");
+static_assert(sizeof(UpdScratch::KA) >= 28 * sizeof(double), "St16 col / f");
+static_assert(offsetof(UpdScratch, hj) == offsetof(UpdScratch, Mjj) + sizeof(UpdScratch::Mjj) &&
+              offsetof(UpdScratch, cen) == offsetof(UpdScratch, hj) + sizeof(UpdScratch::hj) &&
+              sizeof(UpdScratch::Mjj) + sizeof(UpdScratch::hj) + sizeof(UpdScratch::cen) >= 72 * sizeof(double), "St16 Ct");
 
 struct QpScratch {
     static constexpr int N = NQ;
@@ -410,6 +425,7 @@ __device__ __forceinline__ double sel3(const double* v, int k) { return k == 0 ?
 __device__ __forceinline__ double sel4d(int k, double a, double b, double c, double d) {
     return k == 0 ? a : (k == 1 ? b : (k == 2 ? c : d));
 }
+__device__ __forceinline__ double sel3d(int j, double a, double b, double c) { return j == 0 ? a : (j == 1 ? b : c); }
 
 // Diagnostic build only (-DWBC_STAMPS): lane 0 records the shader clock at phase boundaries into
 // the robot's debug record slots WBC_DBG_STAMPS.. (never read by the kernel, never an output).
@@ -1117,6 +1133,335 @@ __device__ bool rank6_factor(const Prob& P, UpdScratch& s, double gsv, int lane)
 }
 
 // ---------------------------------------------------------------------------------------
+// General contact mask: the reference QP (cpp:466-515) reduced exactly to 12
+// variables z, one 3-slot per leg (a swing leg's joint accelerations, a stance leg's force), with
+// only inequality rows (the stance legs' friction faces and the 24 torque rows):
+//   * a = Mb^-1 (E_S^T f - w_g) (R0, cpp:492);
+//   * swing slacks: R4 / R5 (cpp:496-497, 507-515) say s_i >= |r_i|, r_i = Js_i [a; qdd] - rsw_i,
+//     and s_i is in the objective only as 1/2 w s_i^2 (w = slack_weight), so s_i = |r_i| and the
+//     row pair becomes the penalty 1/2 w r_i^2; a stance leg's pair is vacuous (s_i = |rsw_i|);
+//   * stance equalities R1 (cpp:494, 504): Jbj_S qdd + G_S f = e_S, with Jbj = Jblk - E K, solved
+//     for the stance joints by Woodbury as in stance_reduce: qdd_S = q0 + Y phi,
+//     phi = K_W qdd_W - Mb^-1 E_S^T f = B z (column j of B: K_j for a swing slot, -Mb^-1 E_j^T for
+//     a stance slot).
+// The objective becomes 1/2 z^T H z + g^T z with H = I + P^T (I + Mb^-2) P + sum_i w_i Rho_i^T Rho_i,
+// P z = E_S^T f and Rho the 12 "leg rows": a stance joint's acceleration q0_i + Y_i B z (w_i = 1)
+// or a swing foot's task residual r_i = rho0_i + J_l[k] z_l + v_i B z (v_i = -S6^-T E_i^T,
+// rho0_i = E_i c_psi - rsw_i, c_psi = -[0, 0, g, 0, 0, 0] - K_S q0; w_i = slack_weight).  With
+// V = sum_i w_i v_i v_i^T (v_i = Y_i on stance rows), o_a = sum_i w_i own_ia v_i (own_i = J_l[k] on
+// the swing leg's own slot) and blk = w J_l^T J_l (per swing leg):
+//   H_aj = d_aj + blk_aj + (C_P P_a) . P_j + (V B_a + o_a) . B_j + B_a . o_j,
+//   g_a  = -E_a (W + [0, 0, g / m, 0, 0, 0]) (stance) or w sum_k J_l[k][k_a] rho0_(l,k) (swing)
+//          + B_a . gamma,   gamma = sum_i w_i v_i rho0_i.
+// Torques: tau = t0 - Nt z, t0 = bbj + Mbj[:, S] q0, Nt[r][j] = -(Mbj[r, S] Y) . B_j + (stance j:
+// Jbj[j][r]; swing j: -Mbj[r][j]).  Lane i < 12 of the robot's 16-lane segment is leg row / slot /
+// joint i.  Returns false (nothing overwritten in the problem record: the caller takes the general
+// 24-variable path) at a near-singular stance leg, S6 or factor; `vac` is the infeasibility of the
+// swing legs' vacuous R1 rows (quirk A.12: 0 = r1).  Identical for every mask to the literal
+// 42 x 70 QP (oracle/wbc_reduced.py, tests/test_oracle_reduced.py).
+// ---------------------------------------------------------------------------------------
+__device__ bool reduce_general([[maybe_unused]] const KernelArgs& ka, [[maybe_unused]] int rb, Prob& P,
+                               const wbc_params& pr, int lane, int kap, UpdScratch& s, const St16& V, bool& vac) {
+    static_assert(offsetof(UpdScratch, sr) + offsetof(decltype(UpdScratch::sr), Y) >=
+                      offsetof(UpdScratch, ps) + sizeof(UpdScratch::ps), "Y / q0 survive the factorisation");
+    auto& R = s.sr;
+    const int i = lane < 12 ? lane : 11, l = i / 3, k = i % 3;
+    const bool sti = (kap >> l) & 1;
+    const double dl[3] = {P.d[3 * l], P.d[3 * l + 1], P.d[3 * l + 2]};
+    const double inv_m = P.inv_m;
+    const double wsw = pr.slack_weight;
+    // vacuous rows: a swing leg's R1 row reads 0 = r1
+    vac = seg_any<16>(lane < 12 && !sti && fabs(P.r1[i]) > 1e-9 * fmax(1.0, fabs(P.r1[i])));
+    // R1: row k of J_l^-1 for a stance leg (W row i = [jr, d_l x jr], w_i = jr . e_l); swing rows 0
+    bool ok;
+    {
+        const double* A = s.Jf[l];
+        const double c00 = A[4] * A[8] - A[5] * A[7], c01 = A[5] * A[6] - A[3] * A[8], c02 = A[3] * A[7] - A[4] * A[6];
+        const double det = A[0] * c00 + A[1] * c01 + A[2] * c02;
+        double amx = 0.0;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) amx = fmax(amx, fabs(A[t]));
+        ok = !sti || fabs(det) > 1e-9 * amx * amx * amx;
+        const double id = sti ? fast_rcp(ok ? det : 1.0) : 0.0;
+        const double r0[3] = {c00, A[2] * A[7] - A[1] * A[8], A[1] * A[5] - A[2] * A[4]};
+        const double r1[3] = {c01, A[0] * A[8] - A[2] * A[6], A[2] * A[3] - A[0] * A[5]};
+        const double r2[3] = {c02, A[1] * A[6] - A[0] * A[7], A[0] * A[4] - A[1] * A[3]};
+        double jr[3];
+#pragma unroll
+        for (int t = 0; t < 3; ++t) jr[t] = ((k == 0) ? r0[t] : (k == 1) ? r1[t] : r2[t]) * id;
+        if (lane < 12) {
+            double dxj[3];
+            cross3(dl, jr, dxj);
+            double wi = 0.0;
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                R.W[i][t] = jr[t];
+                R.W[i][3 + t] = dxj[t];
+                wi = fma(jr[t], P.r1[3 * l + t] + (t == 2 ? pr.gravity : 0.0), wi);
+            }
+            R.w[i] = wi;
+        }
+    }
+    lds_sync();
+    // R2: [S6 | z6] = [I - K W | K w] (42 entries in one round over 12 lanes, as stance_reduce)
+    {
+        const int ra = lane % 6, h = (lane / 6) & 1;
+        double acc[4][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+            const double kj = (ra < 3) ? s.A[j][ra] * inv_m : s.KA[j][ra < 3 ? 0 : ra - 3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) acc[c][j & 3] = fma(kj, R.W[j][3 * h + c], acc[c][j & 3]);
+            acc[3][j & 3] = fma(kj, R.w[j], acc[3][j & 3]);
+        }
+        if (lane < 12) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const int cb = 3 * h + c;
+                R.S[ra][cb] = (ra == cb ? 1.0 : 0.0) - ((acc[c][0] + acc[c][1]) + (acc[c][2] + acc[c][3]));
+            }
+            if (h) R.S[ra][6] = (acc[3][0] + acc[3][1]) + (acc[3][2] + acc[3][3]);
+        }
+    }
+    lds_sync();
+    // R3: S6^-1 by Gauss-Jordan without pivoting (S6 = I without stance legs; cond < 10 otherwise)
+    {
+        const int r = lane < 6 ? lane : 5;
+        double sr_[6], ir[6];
+        double smx = 0.0;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+            sr_[c] = R.S[r][c];
+            ir[c] = (r == c) ? 1.0 : 0.0;
+        }
+#pragma unroll
+        for (int c = 0; c < 6; ++c)
+#pragma unroll
+            for (int rr = 0; rr < 6; ++rr) smx = fmax(smx, fabs(R.S[rr][c]));
+        double pmin = 1e300;
+#pragma unroll
+        for (int kk = 0; kk < 6; ++kk) {
+            const double pv = seg_bcast<16>(sr_[kk], kk);
+            pmin = fmin(pmin, fabs(pv));
+            const double ip = fast_rcp(pv);
+            double prow[12];
+#pragma unroll
+            for (int c = kk + 1; c < 6; ++c) prow[c] = seg_bcast<16>(sr_[c], kk);
+#pragma unroll
+            for (int c = 0; c <= kk; ++c) prow[6 + c] = seg_bcast<16>(ir[c], kk);
+            const double f = (lane == kk) ? 0.0 : sr_[kk] * ip;
+            const double own = (lane == kk) ? ip : 1.0;
+#pragma unroll
+            for (int c = kk + 1; c < 6; ++c) sr_[c] = fma(-f, prow[c], sr_[c] * own);
+#pragma unroll
+            for (int c = 0; c <= kk; ++c) ir[c] = fma(-f, prow[6 + c], ir[c] * own);
+        }
+        ok = ok && pmin > 1e-6 * smx;
+        if (lane < 6) {
+#pragma unroll
+            for (int c = 0; c < 6; ++c) R.Si[lane][c] = ir[c];
+        }
+    }
+    ok = !seg_any<16>(!ok);
+    lds_sync();
+    if (!ok) return false;
+    // R4: Y_i = W_i S6^-1, q0_i = w_i + Y_i z6 (zero on swing rows); per lane: B_i, v_i, rho0_i
+    double Bi[6], Ei[6];  // column i of B, E_i^T = [e_k; row k of -S(d_l)]
+    {
+        double wrow[6], yi[6];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) wrow[c] = R.W[i][c];
+        double q = R.w[i];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+            double a4[2] = {0.0, 0.0};
+#pragma unroll
+            for (int t = 0; t < 6; ++t) a4[t & 1] = fma(wrow[t], R.Si[t][c], a4[t & 1]);
+            yi[c] = a4[0] + a4[1];
+            q = fma(yi[c], R.S[c][6], q);
+        }
+        double pkv[3];
+        pk3(k, dl, pkv);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { Ei[c] = (c == k) ? 1.0 : 0.0; Ei[3 + c] = pkv[c]; }
+        double Ki[6];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { Ki[c] = s.A[i][c] * inv_m; Ki[3 + c] = s.KA[i][c]; }
+        // c_psi = -[0, 0, g, 0, 0, 0] - sum over stance joints of K_j q0_j
+        double cpsi[6];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) cpsi[c] = -seg_sum<16>(lane < 12 ? Ki[c] * q : 0.0) - (c == 2 ? pr.gravity : 0.0);
+        double mpk[3];  // I_c^-1 (row k of -S(d_l))
+        mv3(P.Icinv, pkv, mpk);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            Bi[c] = sti ? -Ei[c] * inv_m : Ki[c];
+            Bi[3 + c] = sti ? -mpk[c] : Ki[3 + c];
+        }
+        // swing row: v_i = -S6^-T E_i^T, rho0_i = E_i c_psi - rsw_i
+        double vi[6];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+            double t = 0.0;
+#pragma unroll
+            for (int b = 0; b < 6; ++b) t = fma(R.Si[b][c], Ei[b], t);
+            vi[c] = sti ? yi[c] : -t;
+        }
+        double ec = 0.0;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) ec = fma(Ei[c], cpsi[c], ec);
+        const double rho = sti ? q : ec - P.rsw[i];
+        if (lane < 12) {
+#pragma unroll
+            for (int c = 0; c < 6; c += 2) {
+                *reinterpret_cast<double2*>(&R.Y[i][c]) = make_double2(yi[c], yi[c + 1]);
+                *reinterpret_cast<double2*>(&V.Vt[i * 6 + c]) = make_double2(vi[c], vi[c + 1]);
+                *reinterpret_cast<double2*>(&V.Bt[i * 6 + c]) = make_double2(Bi[c], Bi[c + 1]);
+            }
+            R.q0[i] = q;
+            V.rho0[i] = rho;
+        }
+    }
+    lds_sync();
+    UST(ka, rb, 20);
+    // R5: [V | gamma] = sum_j w_j v_j [v_j^T | rho0_j] (42 entries in one round); slot a's o_a,
+    // its blk row and its own gradient term (swing)
+    {
+        const int ra = lane % 6, h = (lane / 6) & 1;
+        double acc[4][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+            const double wj = ((kap >> (j / 3)) & 1) ? 1.0 : wsw;
+            const double vj = wj * V.Vt[j * 6 + ra];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) acc[c][j & 3] = fma(vj, V.Vt[j * 6 + 3 * h + c], acc[c][j & 3]);
+            acc[3][j & 3] = fma(vj, V.rho0[j], acc[3][j & 3]);
+        }
+        if (lane < 12) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) R.Q[ra][3 * h + c] = (acc[c][0] + acc[c][1]) + (acc[c][2] + acc[c][3]);
+            if (h) R.Q[ra][6] = (acc[3][0] + acc[3][1]) + (acc[3][2] + acc[3][3]);
+        }
+    }
+    double blk[3] = {0.0, 0.0, 0.0}, gown = 0.0;
+    {
+        // o_a = w sum_r J_l[r][k] v_(l,r) (swing slot a = (l, k)); stance slot: C_a = P_a = E_a^T
+        double oa[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            const double jrk = s.Jf[l][3 * r + k];
+#pragma unroll
+            for (int c = 0; c < 6; ++c) oa[c] = fma(jrk, V.Vt[(3 * l + r) * 6 + c], oa[c]);
+#pragma unroll
+            for (int kj = 0; kj < 3; ++kj) blk[kj] = fma(jrk, s.Jf[l][3 * r + kj], blk[kj]);
+            gown = fma(jrk, V.rho0[3 * l + r], gown);
+        }
+        if (lane < 12) {
+#pragma unroll
+            for (int c = 0; c < 6; c += 2)
+                *reinterpret_cast<double2*>(&V.Ct[i * 6 + c]) =
+                    make_double2(sti ? Ei[c] : wsw * oa[c], sti ? Ei[c + 1] : wsw * oa[c + 1]);
+        }
+    }
+    lds_sync();
+    UST(ka, rb, 21);
+    // R6: H row a = i and g_a
+    double hrow[12], gsv;
+    {
+        double al[6], be[6];
+        // alpha_a = (I + Mb^-2) P_a (stance), 0 (swing)
+        {
+            double t[3], t2[3];
+            mv3(P.Icinv, &Ei[3], t);
+            mv3(P.Icinv, t, t2);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                al[c] = sti ? Ei[c] * (1.0 + inv_m * inv_m) : 0.0;
+                al[3 + c] = sti ? Ei[3 + c] + t2[c] : 0.0;
+            }
+        }
+        // beta_a = V B_a + o_a
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+            double t = sti ? 0.0 : V.Ct[i * 6 + c];
+#pragma unroll
+            for (int b = 0; b < 6; ++b) t = fma(R.Q[c][b], Bi[b], t);
+            be[c] = t;
+        }
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+            const bool stj = (kap >> (j / 3)) & 1;
+            double bj[6], cj[6];
+#pragma unroll
+            for (int c = 0; c < 6; c += 2) {
+                const double2 b2 = *reinterpret_cast<const double2*>(&V.Bt[j * 6 + c]);
+                const double2 c2 = *reinterpret_cast<const double2*>(&V.Ct[j * 6 + c]);
+                bj[c] = b2.x; bj[c + 1] = b2.y; cj[c] = c2.x; cj[c + 1] = c2.y;
+            }
+            double h = (i == j) ? 1.0 : 0.0;
+            if (!sti && j / 3 == l) h = fma(wsw, sel3d(j % 3, blk[0], blk[1], blk[2]), h);
+            double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+            for (int c = 0; c < 6; ++c) {
+                t1 = fma(be[c], bj[c], t1);
+                t2 = fma(stj ? al[c] : Bi[c], cj[c], t2);
+            }
+            hrow[j] = h + t1 + t2;
+        }
+        double gam = 0.0;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) gam = fma(Bi[c], R.Q[c][6], gam);
+        double wv[6];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) wv[c] = P.W[c] + (c == 2 ? pr.gravity * inv_m : 0.0);
+        double ew = 0.0;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) ew = fma(Ei[c], wv[c], ew);
+        gsv = (sti ? -ew : wsw * gown) + gam;
+    }
+    UST(ka, rb, 22);
+    // R7: H = L L^T, M = L^-1, x0 = -H^-1 g (ps.L, ps.xs: over W .. Si, all read by now)
+    lds_sync();
+    ok = factor12<16>(hrow, gsv, lane, s.ps.L, s.ps.ild, s.ps.xs);
+    if (!ok) return false;
+    // R8: torque map row r = i, t0_r, the row's reference-space norm; then Nt over Jbj
+    {
+        const int r = i;
+        double my[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, t4[2] = {0.0, 0.0}, s2 = 0.0, mrow[12];
+#pragma unroll
+        for (int kk = 0; kk < 12; ++kk) {
+            const double mk = P.Mbj[r * 12 + kk];
+            const bool stk = (kap >> (kk / 3)) & 1;
+            const double jc = stk ? P.Jbj[kk * 12 + r] : 0.0;
+            mrow[kk] = stk ? jc : -mk;  // the slot's own term of Nt[r][kk]
+#pragma unroll
+            for (int c = 0; c < 6; ++c) my[c] = fma(mk, R.Y[kk][c], my[c]);
+            t4[kk & 1] = fma(mk, R.q0[kk], t4[kk & 1]);
+            s2 = fma(mk, mk, fma(jc, jc, s2));
+        }
+        double nt[12];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+            double t = mrow[j];
+#pragma unroll
+            for (int c = 0; c < 6; ++c) t = fma(-my[c], V.Bt[j * 6 + c], t);
+            nt[j] = t;
+        }
+        const double t0v = P.bbj[r] + (t4[0] + t4[1]);
+        lds_sync();  // every lane has read Jbj / Mbj
+        if (lane < 12) {
+#pragma unroll
+            for (int c = 0; c < 12; c += 2) *reinterpret_cast<double2*>(&V.Nt[r * 12 + c]) = make_double2(nt[c], nt[c + 1]);
+            V.t0[r] = t0v;
+            V.nsel[r] = s2;
+        }
+    }
+    lds_sync();
+    UST(ka, rb, 14);
+    return true;
+}
+
+// ---------------------------------------------------------------------------------------
 // inline stance solve: the 12-variable force-space QP of a four-contact robot whose equalities
 // stance_reduce eliminated, solved by its own 16-lane segment of the update wave (four robots per
 // wave) right after factor12, so that nothing of it passes through HBM.  The Goldfarb-Idnani
@@ -1153,23 +1498,26 @@ __device__ __forceinline__ double seg_shfl(double v, int j) { return vbcast(v, (
 __device__ __forceinline__ int seg_shfl_i(int v, int j) {
     return __builtin_amdgcn_ds_bpermute((((int)threadIdx.x & ~15) + (j & 15)) << 2, v);
 }
-__device__ __forceinline__ double sel3d(int j, double a, double b, double c) { return j == 0 ? a : (j == 1 ? b : c); }
 
-// ROWS: the J mirror already holds J0 by rows (rank6_factor); otherwise M = L^-1 (factor12)
-template <bool ROWS>
-__device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, const Prob& P, UpdScratch& s) {
+// ROWS: the J mirror already holds J0 by rows (rank6_factor); otherwise M = L^-1 (factor12).
+// GEN: the general form of any contact mask (reduce_general, St16(s, P)): friction rows only for
+// stance legs, the hotstart of stateful steps, the outputs mapped back through B, Y and the leg
+// rows; otherwise the four-contact stance form (stateless).  qp = output row, hr = history row.
+template <bool ROWS, bool GEN>
+__device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, const Prob& P, UpdScratch& s,
+                        const St16& V, int kap, int status0) {
     constexpr int N = 12;
     const wbc_params& pr = a.pv;
-    const St16 V(s);
     double* Jl = &s.ps.L[0][0];  // M = L^-1 (row-major 12 x 12) on entry, then the LDS mirror of J
     const int i = l < N ? l : 0;
-    int status = (P.flags != 0.0) ? WBC_QP_NUMERIC : WBC_QP_OK;
+    int status = (P.flags != 0.0) ? WBC_QP_NUMERIC : status0;
     int iters = 0;
     lds_sync();
 
     // normals (force space) of the three slots, as solve_stance / build_normal
     const int fl = l >> 2, rr = l & 3, k1 = l >> 1, k2 = 8 + ((l & 7) >> 1);
     const bool v2 = l < 8;
+    const bool fon = GEN ? (((kap >> fl) & 1) != 0) : true;  // friction faces exist for stance legs only
     const double sg = (l & 1) ? -1.0 : 1.0;
     double n0[N], n1[N], n2[N];
 #pragma unroll
@@ -1188,20 +1536,25 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
     const double in0 = 1.0 / sqrt(fmax(1.0 + pr.friction * pr.friction, 1e-300));
     const double in1 = 1.0 / sqrt(fmax(V.nsel[k1], 1e-300)), in2 = 1.0 / sqrt(fmax(V.nsel[k2], 1e-300));
     double sp0, sp1, sp2;
-    {
+    auto slacks = [&](const double* xv) {
         double q0[4] = {0.0, 0.0, 0.0, 0.0}, q1[4] = {0.0, 0.0, 0.0, 0.0}, q2[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int j = 0; j < N; ++j) {
-            const double xv = s.ps.xs[j];
-            q0[j & 3] += n0[j] * xv;
-            q1[j & 3] += n1[j] * xv;
-            q2[j & 3] += n2[j] * xv;
+            q0[j & 3] += n0[j] * xv[j];
+            q1[j & 3] += n1[j] * xv[j];
+            q2[j & 3] += n2[j] * xv[j];
         }
         sp0 = ((q0[0] + q0[1]) + (q0[2] + q0[3])) - 0.0;
         sp1 = ((q1[0] + q1[1]) + (q1[2] + q1[3])) - bp1;
         sp2 = ((q2[0] + q2[1]) + (q2[2] + q2[3])) - bp2;
+    };
+    {
+        double xv[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) xv[j] = s.ps.xs[j];
+        slacks(xv);
     }
-    // J = L^-T (row l of J = column l of M in lane l < 12), the primal x = f0 (x_l in lane l)
+    // J = L^-T (row l of J = column l of M in lane l < 12), the primal x = x0 (x_l in lane l)
     double Jr[N];
 #pragma unroll
     for (int j = 0; j < N; ++j) Jr[j] = (l < N) ? (ROWS ? Jl[i * 12 + j] : Jl[j * 12 + i]) : 0.0;
@@ -1224,10 +1577,160 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
     double u = 0.0, up = 0.0;
     bool done = (status != WBC_QP_OK);
     const int max_wsr = pr.max_wsr;
+
+    // d = J^T n (lane j: column j of the mirror . n), broadcast to every lane; d2 = rows >= pos;
+    // r = R^-1 d (lane l < q), zn = |d2|^2, z = J2 d2 (lane k: z_k), dq = d[pos], jq = J[l][pos]
+    auto direction = [&](const double* jc, const double* np, int pos, double* d2, double& rk, double& zn, double& zk,
+                         double& dq, double& jq) {
+        double dj;
+        {
+            double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int k = 0; k < N; ++k) acc[k & 3] += jc[k] * np[k];
+            dj = (l < N) ? (acc[0] + acc[1]) + (acc[2] + acc[3]) : 0.0;
+        }
+        lds_sync();
+        double d[N];
+#pragma unroll
+        for (int k = 0; k < N; ++k) d[k] = seg_bcast<16>(dj, k);
+        // d[pos] and J[l][pos] (needed only by the Householder add, so their LDS latency is off
+        // the chain): from lane pos of the segment and from the J mirror
+        dq = seg_shfl(dj, pos);  // lane 12.. holds 0
+        jq = (l >= N || pos >= N) ? 0.0 : Jl[i * 12 + (pos < N ? pos : 0)];
+        {
+            double acc[4] = {0.0, 0.0, 0.0, 0.0}, zz[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                const double mk = (j >= pos) ? 1.0 : 0.0;
+                acc[j & 3] += rinv[j] * d[j];
+                d2[j] = d[j] * mk;
+                zz[j & 3] += d[j] * d2[j];
+            }
+            rk = (l < N) ? (acc[0] + acc[1]) + (acc[2] + acc[3]) : 0.0;
+            zn = (zz[0] + zz[1]) + (zz[2] + zz[3]);
+        }
+        {
+            double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int j = 0; j < N; ++j) acc[j & 3] += Jr[j] * d2[j];
+            zk = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+        }
+    };
+    // Householder add at slot pos: J <- J H on columns pos.. (row l: v . J_l = z_l - alpha J_l[pos]);
+    // R^-1 gains the column [-r / alpha; 1 / alpha]
+    auto householder_add = [&](int pos, const double* d2, double rk, double zn, double zk, double dq, double jq) {
+        const double rs = fast_rsq(zn);
+        const double nrm2 = zn * rs;
+        const double alpha = (dq >= 0.0) ? -nrm2 : nrm2;
+        const double ia = (dq >= 0.0) ? -rs : rs;
+        const double beta = fast_rcp(zn + nrm2 * fabs(dq));
+        const double vw = (zk - alpha * jq) * beta, vwa = vw * alpha;
+#pragma unroll
+        for (int k = 0; k < N; ++k) Jr[k] = fma(vwa, (k == pos) ? 1.0 : 0.0, fma(-vw, d2[k], Jr[k]));
+        const double nv = (l == pos) ? ia : -rk * ia;
+        // column pos of R^-1 is 0 before the add and nv is finite here (zn > 1e-14), so adding nv
+        // under the 0 / 1 mask is exact
+        const double nvw = (l <= pos) ? nv : 0.0;
+#pragma unroll
+        for (int k = 0; k < N; ++k) rinv[k] = fma((k == pos) ? 1.0 : 0.0, nvw, rinv[k]);
+    };
+
+    // Hotstart (qpOASES SQProblem::hotstart, cpp:529-533): the previous solve's working set (row
+    // ids of this numbering, tagged 16 + mask in H_WSKAP) minus the friction rows of legs that are
+    // no longer in contact, re-added as a block without steps (the mirror's columns), then the
+    // point where every warm row holds with equality: v = -R^-T s_A(x0), u = R^-1 v, x = x0 + J v.
+    // A dependent warm row or a multiplier below -1e-10 rejects the set: cold start from x0.
+    if constexpr (GEN) {
+        if (!done && a.stateful && !a.cold) {
+            const double* H = a.hist + (size_t)rb * HIST_LEN;
+            const double tag = H[H_WSKAP];
+            unsigned long long ws = (tag >= 16.0) ? ((unsigned long long)(unsigned)H[H_WSLO] |
+                                                     ((unsigned long long)(unsigned)H[H_WSHI] << 32))
+                                                  : 0ull;
+            unsigned long long keep = 0xFFFFFFull << 16;  // torque rows
+#pragma unroll
+            for (int lg = 0; lg < 4; ++lg)
+                if ((kap >> lg) & 1) keep |= 0xFull << (4 * lg);
+            ws &= keep;
+            const int nw = __popcll(ws);
+            if (nw > 0 && nw <= N) {
+                if (l < N) {  // J0 for a rejection
+#pragma unroll
+                    for (int j = 0; j < N; j += 2) *reinterpret_cast<double2*>(&V.J0[i * 12 + j]) = make_double2(Jr[j], Jr[j + 1]);
+                }
+                bool fail = false;
+                unsigned long long rem = ws;
+                for (int w = 0; w < nw; ++w) {
+                    const int p = __builtin_ctzll(rem);
+                    rem &= rem - 1ull;
+                    const int ol = p & 15, js = p >> 4, pos = q;
+                    double jc[N];
+#pragma unroll
+                    for (int k = 0; k < N; ++k) jc[k] = Jl[k * 12 + i];
+                    if (l == ol) {
+#pragma unroll
+                        for (int k = 0; k < N; ++k) V.col[k] = sel3d(js, n0[k], n1[k], n2[k]);
+                    }
+                    lds_sync();
+                    double np[N], nn = 0.0;
+#pragma unroll
+                    for (int k = 0; k < N; ++k) { np[k] = V.col[k]; nn = fma(np[k], np[k], nn); }
+                    double d2[N], rk, zn, zk, dq, jq;
+                    direction(jc, np, pos, d2, rk, zn, zk, dq, jq);
+                    if (!(zn > 1e-26 * fmax(1.0, nn))) { fail = true; break; }  // dependent: reject
+                    householder_add(pos, d2, rk, zn, zk, dq, jq);
+                    if (l == pos) act = p;
+                    if (l == ol) ab |= 1 << js;
+                    ++q;
+                    mirror();
+                }
+                if (!fail) {
+                    // slack at x0 of the row in slot l (from its owner lane), then v, u, x
+                    const int ow = act < 0 ? 0 : act & 15, jw = act < 0 ? 0 : act >> 4;
+                    const double o0 = seg_shfl(sp0, ow), o1 = seg_shfl(sp1, ow), o2 = seg_shfl(sp2, ow);
+                    const double sk = (l < q) ? sel3d(jw, o0, o1, o2) : 0.0;
+                    double v[N];
+#pragma unroll
+                    for (int j = 0; j < N; ++j) v[j] = -seg_sum<16>(l < q ? rinv[j] * sk : 0.0);
+                    double uu[4] = {0.0, 0.0, 0.0, 0.0}, xx[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                    for (int j = 0; j < N; ++j) {
+                        uu[j & 3] = fma(rinv[j], v[j], uu[j & 3]);
+                        xx[j & 3] = fma(Jr[j], v[j], xx[j & 3]);
+                    }
+                    const double uw = (uu[0] + uu[1]) + (uu[2] + uu[3]);
+                    fail = seg_any<16>(l < q && uw < -1e-10);
+                    if (!fail) {
+                        if (l < q) u = fmax(uw, 0.0);
+                        if (l < N) x += (xx[0] + xx[1]) + (xx[2] + xx[3]);
+                        double xv[N];
+#pragma unroll
+                        for (int j = 0; j < N; ++j) xv[j] = seg_bcast<16>(x, j);
+                        slacks(xv);
+                    }
+                }
+                if (fail) {  // back to the cold start: J0, empty working set, x0 and its slacks
+                    lds_sync();
+#pragma unroll
+                    for (int j = 0; j < N; ++j) Jr[j] = (l < N) ? V.J0[i * 12 + j] : 0.0;
+#pragma unroll
+                    for (int k = 0; k < N; ++k) rinv[k] = 0.0;
+                    q = 0; act = -1; ab = 0; u = 0.0;
+                    x = (l < N) ? s.ps.xs[i] : 0.0;
+                    double xv[N];
+#pragma unroll
+                    for (int j = 0; j < N; ++j) xv[j] = s.ps.xs[j];
+                    slacks(xv);
+                    mirror();
+                }
+            }
+        }
+    }
+
     // most violated row, by slack / |reference row| (ties to the lowest row); none: optimal.  Run
     // before the loop and then right after each add, where it overlaps the Householder update of J
     auto select = [&]() {
-        const double w0 = (!(ab & 1) && sp0 < -tol0) ? sp0 * in0 : 1e300;
+        const double w0 = (fon && !(ab & 1) && sp0 < -tol0) ? sp0 * in0 : 1e300;
         const double w1 = (!(ab & 2) && sp1 < -tol1) ? sp1 * in1 : 1e300;
         const double w2 = (v2 && !(ab & 4) && sp2 < -tol2) ? sp2 * in2 : 1e300;
         const double m = seg16_min(fmin(tag6(w0, l), fmin(tag6(w1, 16 + l), tag6(w2, 32 + l))));
@@ -1255,44 +1758,9 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
 #pragma unroll
             for (int k = 0; k < N; ++k) np[k] = V.col[k];
             const double sps = V.col[12];
-            // d = J^T n+ (lane j: column j of the mirror), then to every lane
-            double dj;
-            {
-                double acc[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                for (int k = 0; k < N; ++k) acc[k & 3] += jc[k] * np[k];
-                dj = (l < N) ? (acc[0] + acc[1]) + (acc[2] + acc[3]) : 0.0;
-            }
-            lds_sync();
-            double d[N], d2[N];
-#pragma unroll
-            for (int k = 0; k < N; ++k) d[k] = seg_bcast<16>(dj, k);
-            // d[pos] and J[l][pos] (needed only by the Householder add, so their LDS latency is
-            // off the chain): from lane pos of the segment and from the J mirror, instead of
-            // 12-term sums against a 0 / 1 row mask (pos varies by segment)
-            const double dq = seg_shfl(dj, pos);  // lane 12.. holds 0
-            const double jq = (l >= N || pos >= N) ? 0.0 : Jl[i * 12 + (pos < N ? pos : 0)];
-            double rk, zn;
-            {
-                double acc[4] = {0.0, 0.0, 0.0, 0.0}, zz[4] = {0, 0, 0, 0};
-#pragma unroll
-                for (int j = 0; j < N; ++j) {
-                    const double mk = (j >= pos) ? 1.0 : 0.0;
-                    acc[j & 3] += rinv[j] * d[j];
-                    d2[j] = d[j] * mk;
-                    zz[j & 3] += d[j] * d2[j];
-                }
-                rk = (l < N) ? (acc[0] + acc[1]) + (acc[2] + acc[3]) : 0.0;
-                zn = (zz[0] + zz[1]) + (zz[2] + zz[3]);
-            }
-            // primal direction z = J2 d2 (lane k: z_k), then to every lane; slack rates n . z
-            double zk;
-            {
-                double acc[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                for (int j = 0; j < N; ++j) acc[j & 3] += Jr[j] * d2[j];
-                zk = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-            }
+            double d2[N], rk, zn, zk, dq, jq;
+            direction(jc, np, pos, d2, rk, zn, zk, dq, jq);
+            // slack rates n . z of the lane's rows (z_m broadcast from lane m)
             double cz0, cz1, cz2;
             {
                 double z0[4] = {0, 0, 0, 0}, z1[4] = {0, 0, 0, 0}, z2[4] = {0, 0, 0, 0};
@@ -1329,22 +1797,7 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
                     if (l == ol) ab |= 1 << js;
                     ++q;
                     select();  // the next row: slacks and active flags are final, J is not needed
-                    // Householder add: J <- J H on columns pos.. (row l: v . J_l = z_l - alpha J_l[pos]);
-                    // R^-1 gains the column [-r / alpha; 1 / alpha]
-                    const double rs = fast_rsq(zn);
-                    const double nrm2 = zn * rs;
-                    const double alpha = (dq >= 0.0) ? -nrm2 : nrm2;
-                    const double ia = (dq >= 0.0) ? -rs : rs;
-                    const double beta = fast_rcp(zn + nrm2 * fabs(dq));
-                    const double vw = (zk - alpha * jq) * beta, vwa = vw * alpha;
-#pragma unroll
-                    for (int k = 0; k < N; ++k) Jr[k] = fma(vwa, (k == pos) ? 1.0 : 0.0, fma(-vw, d2[k], Jr[k]));
-                    const double nv = (l == pos) ? ia : -rk * ia;
-                    // column pos of R^-1 is 0 before the add and nv is finite here (zn > 1e-14),
-                    // so adding nv under the 0 / 1 mask is exact
-                    const double nvw = (l <= pos) ? nv : 0.0;
-#pragma unroll
-                    for (int k = 0; k < N; ++k) rinv[k] = fma((k == pos) ? 1.0 : 0.0, nvw, rinv[k]);
+                    householder_add(pos, d2, rk, zn, zk, dq, jq);
                 } else {
                     // drop slot l1: shift the active lists, then Givens deletion (givens_drop) with the
                     // rotation of step k from the R column of the row now in slot k: (J^T n)[k, k+1]
@@ -1395,46 +1848,88 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
     lds_sync();
     UST(a, rb, 17);  // primal
     const bool ok = (status == WBC_QP_OK);
-    if (wr && l < N) {  // tau_j = t0_j - Nt_j f (cpp:565-576), grf = f (cpp:556-563)
+    const bool stl = GEN ? (((kap >> (i / 3)) & 1) != 0) : true;  // slot i is a stance force
+    if (wr && l < N) {  // tau_j = t0_j - Nt_j z (cpp:565-576), grf = f (cpp:556-563)
         double t4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int c = 0; c < 12; ++c) t4[c & 3] = fma(V.Nt[l * 12 + c], V.f[c], t4[c & 3]);
         const double tv = V.t0[l] - ((t4[0] + t4[1]) + (t4[2] + t4[3]));
-        a.tau[(size_t)rb * 12 + l] = ok ? tv : 0.0;
-        a.grf[(size_t)rb * 12 + l] = ok ? V.f[l] : 0.0;
+        a.tau[(size_t)qp * 12 + l] = ok ? tv : 0.0;
+        a.grf[(size_t)qp * 12 + l] = (ok && stl) ? V.f[l] : 0.0;
     }
-    if (a.x && wr) {  // x (42, cpp:534-541): a = Mb^-1 (E^T f - gw), qdd = q0 - Y Mb^-1 E^T f, f, |rsw|
+    if (a.x && wr) {  // x (42, cpp:534-541): a = Mb^-1 (E_S^T f) - g e_z, qdd, f, slacks
         double F[3] = {0, 0, 0}, Mm[3] = {0, 0, 0};
 #pragma unroll
         for (int ll = 0; ll < 4; ++ll) {
-            const double fv[3] = {V.f[3 * ll], V.f[3 * ll + 1], V.f[3 * ll + 2]};
+            const bool st = GEN ? (((kap >> ll) & 1) != 0) : true;
+            const double fv[3] = {st ? V.f[3 * ll] : 0.0, st ? V.f[3 * ll + 1] : 0.0, st ? V.f[3 * ll + 2] : 0.0};
             const double dl[3] = {P.d[3 * ll], P.d[3 * ll + 1], P.d[3 * ll + 2]};
             double t[3];
             cross3(dl, fv, t);
 #pragma unroll
             for (int c = 0; c < 3; ++c) { F[c] += fv[c]; Mm[c] += t[c]; }
         }
-        double bf[6];
+        double bf[6];  // Mb^-1 E_S^T f
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             bf[c] = F[c] * P.inv_m;
             bf[3 + c] = P.Icinv[3 * c] * Mm[0] + P.Icinv[3 * c + 1] * Mm[1] + P.Icinv[3 * c + 2] * Mm[2];
         }
+        // phi = B z (general); the stance form's phi = -Mb^-1 E^T f
+        double phi[6];
+        if constexpr (GEN) {
+#pragma unroll
+            for (int c = 0; c < 6; ++c) phi[c] = 0.0;
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                const double zj = V.f[j];
+#pragma unroll
+                for (int c = 0; c < 6; ++c) phi[c] = fma(V.Bt[j * 6 + c], zj, phi[c]);
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < 6; ++c) phi[c] = -bf[c];
+        }
         if (l < 12) {
-            double* xr = a.x + (size_t)rb * WBC_NV;
+            double* xr = a.x + (size_t)qp * WBC_NV;
             if (l < 6) xr[l] = ok ? ((l < 3) ? sel3(bf, l < 3 ? l : 0) - (l == 2 ? pr.gravity : 0.0)
                                              : sel3(&bf[3], l < 3 ? 0 : l - 3)) : 0.0;
             double qv = V.q0[l];
 #pragma unroll
-            for (int c = 0; c < 6; ++c) qv = fma(-V.Y[l * 6 + c], bf[c], qv);
+            for (int c = 0; c < 6; ++c) qv = fma(V.Y[l * 6 + c], phi[c], qv);
+            double sv = fabs(P.rsw[l]);
+            if constexpr (GEN) {
+                if (!stl) {  // swing: qdd_l is the variable, s = |r| of the foot's task row
+                    qv = V.f[l];
+                    const int lg = l / 3, kk = l % 3;
+                    double r = V.rho0[l];
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) r = fma(s.Jf[lg][3 * kk + c], V.f[3 * lg + c], r);
+#pragma unroll
+                    for (int c = 0; c < 6; ++c) r = fma(V.Vt[l * 6 + c], phi[c], r);
+                    sv = fabs(r);
+                }
+            }
             xr[6 + l] = ok ? qv : 0.0;
-            xr[18 + l] = ok ? V.f[l] : 0.0;
-            xr[30 + l] = ok ? fabs(P.rsw[l]) : 0.0;
+            xr[18 + l] = (ok && stl) ? V.f[l] : 0.0;
+            xr[30 + l] = ok ? sv : 0.0;
         }
     }
     if (wr && l == 0) {
-        a.status[rb] = status;
-        a.iters[rb] = iters;
+        a.status[qp] = status;
+        a.iters[qp] = iters;
+    }
+    if (GEN && a.stateful && wr) {  // working set for the next cycle's hotstart, this numbering
+        const unsigned long long b0 = __ballot((ab & 1) != 0), b1 = __ballot((ab & 2) != 0), b2 = __ballot((ab & 4) != 0);
+        const int sh = (int)threadIdx.x & 48;
+        const unsigned long long ws = ((b0 >> sh) & 0xFFFFull) | (((b1 >> sh) & 0xFFFFull) << 16) |
+                                      (((b2 >> sh) & 0xFFull) << 32);
+        if (l == 0) {
+            double* H = a.hist + (size_t)rb * HIST_LEN;
+            H[H_WSLO] = ok ? (double)(unsigned)(ws & 0xffffffffull) : 0.0;
+            H[H_WSHI] = ok ? (double)(unsigned)(ws >> 32) : 0.0;
+            H[H_WSKAP] = 16.0 + (double)kap;
+        }
     }
     UST(a, rb, 18);  // outputs
 }
@@ -1445,14 +1940,16 @@ __device__ void solve_stance16(const KernelArgs& a, int rb, int l, bool wr, cons
 // ---------------------------------------------------------------------------------------
 // SUB = lanes per robot (64: one robot per wave; 16 / 32: 4 / 2 robots per wave, each with its
 // own scratch); lane = lane within the robot's segment; wr = false for a padding segment past the
-// batch (computes a duplicate robot, writes nothing to HBM).
-// SOLVE: a four-contact robot whose elimination succeeded is solved here too (solve_stance16) and
-// its Presolve record is not written (wbc_update_solve_kernel; the return value says which).
+// batch (computes a duplicate robot, writes nothing to HBM).  rb = the input / history row, kap its
+// QP's contact mask (a hypothesis' mask under wbc_step_modes), qp = the output row.
+// SOLVE (wbc_step_kernel16, the default wbc_step): the QP is reduced to 12 variables and solved
+// here too (solve16: the four-contact stance form on stateless all-stance waves, the general form
+// otherwise); returns false when the reduction was not usable (the caller writes the problem for
+// the general fallback solve).  !SOLVE: the split update (Prob + Presolve records to HBM).
 template <int SUB, bool SOLVE = false>
-__device__ bool update_phase(const KernelArgs& a, int rb, int lane, bool wr, UpdScratch& s, Prob& P, Presolve* pre,
-                             const wbc_model& md) {
+__device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int lane, bool wr, UpdScratch& s, Prob& P,
+                             Presolve* pre, const wbc_model& md) {
     const wbc_params& pr = a.pv;
-    const int kap = a.contacts[rb];
     const bool switching = a.switching[rb] != 0;
     const bool stateful = a.stateful != 0;
     const bool debug = a.debug != 0;
@@ -1952,7 +2449,8 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
         // leg and the swing bound as for a swing leg; the solve kernel masks them per hypothesis
         // (each is read only for legs of its own kind, so the masked values are bit-identical)
         const double kn = (kap >> l) & 1, ko = (kap_old >> l) & 1;
-        const double kr1 = a.modes ? 1.0 : kn, ksw = a.modes ? 0.0 : kn;
+        const bool unmasked = a.modes && !SOLVE;  // the split update of mode hypotheses
+        const double kr1 = unmasked ? 1.0 : kn, ksw = unmasked ? 0.0 : kn;
         double jc_dot = 0.0, js_dot = 0.0;
         if (!switching) {
             jc_dot = (kr1 * cur - ko * old) / dt;
@@ -2081,25 +2579,38 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int lane, bool wr, Upd
     // masks differ per QP: the stance elimination is formed for every state (the bounds are
     // written unmasked, i.e. as for stance legs, which is exactly the kappa = 15 hypothesis) and
     // the other hypotheses factor their slot Hessian in the solve.
+    if constexpr (SOLVE) {
+        static_assert(SUB == 16, "the inline solve runs in 16-lane segments");
+        // stateless waves whose four robots all have mask 15: the four-contact stance form
+        // (stance_reduce + the rank-6 factor, no Hessian to factor); every other wave: the general
+        // form, per robot (its own mask, a hotstart on stateful steps)
+        if (!stateful && __all(kap == 15)) {
+            double hrow[12], gsv = 0.0;
+            if (stance_reduce<true>(a, rb, P, pr, lane, wr, s, hrow, gsv, nullptr) && rank6_factor(P, s, gsv, lane)) {
+                UST(a, rb, 11);
+                solve16<true, false>(a, rb, qp, lane, wr, P, s, St16(s), 15, WBC_QP_OK);
+                return true;
+            }
+            return false;
+        }
+        const St16 V(s, P);
+        bool vac = false;
+        if (reduce_general(a, rb, P, pr, lane, kap, s, V, vac)) {
+            UST(a, rb, 11);
+            solve16<false, true>(a, rb, qp, lane, wr, P, s, V, kap, vac ? WBC_QP_INFEASIBLE : WBC_QP_OK);
+            return true;
+        }
+        return false;
+    }
     if (pre) {
         double hrow[12], gsv = 0.0;
         bool stance = false;
         if constexpr (SUB == 16) {
             if (a.elim && (kap == 15 || a.modes))
-                stance = stance_reduce<SOLVE>(a, rb, P, pr, lane, wr, s, hrow, gsv, pre);
+                stance = stance_reduce<false>(a, rb, P, pr, lane, wr, s, hrow, gsv, pre);
         }
         const bool fact = stance || !a.modes;
         if (fact) {
-            if constexpr (SOLVE && SUB == 16) {
-                if (stance) {
-                    if (rank6_factor(P, s, gsv, lane)) {
-                        UST(a, rb, 11);
-                        solve_stance16<true>(a, rb, lane, wr, P, s);
-                        return true;
-                    }
-                    stance = false;  // degenerate foot layout: the general path
-                }
-            }
             if (!stance) slot_hessian_row(P, kap, pr, lane, hrow, gsv);
             const bool ok = factor12<SUB>(hrow, gsv, lane, s.ps.L, s.ps.ild, s.ps.xs, &a, rb);
             const double (&Mi)[12][12] = *reinterpret_cast<const double(*)[12][12]>(&s.ps.L[0][0]);
@@ -3341,7 +3852,7 @@ WBC_KERNEL_ATTR void wbc_step_kernel(KernelArgs a) {
     const int rb = xcd_robot();
     if (rb >= a.batch) return;
     STAMP(a, rb, 0);
-    update_phase<64>(a, rb, lane_id(), true, L.u, L.prob, nullptr, *a.model);
+    update_phase<64>(a, rb, rb, a.contacts[rb], lane_id(), true, L.u, L.prob, nullptr, *a.model);
     STAMP(a, rb, 1);
     solve_phase(a, rb, L.prob, nullptr, L.q);
     STAMP(a, rb, 6);
@@ -3391,8 +3902,9 @@ __device__ __forceinline__ void stage_to_lds(double2* dst, const double2* src, i
     }
 }
 
-template <bool SOLVE>
-__device__ __forceinline__ void update_kernel_body(const KernelArgs& a) {
+// The split update (wbc_update, WBC_SPLIT, the update of wbc_step_modes' split form): Prob +
+// Presolve records to HBM for wbc_solve_kernel / wbc_solve_stance_kernel.
+WBC_UPDATE_KERNEL_ATTR void wbc_update_kernel(KernelArgs a) {
     __shared__ UpdLds L;
     const int seg = (int)threadIdx.x / UPD_SUB, lane = (int)threadIdx.x % UPD_SUB;
     int rb = (int)blockIdx.x * UPD_RPW + seg;
@@ -3404,10 +3916,11 @@ __device__ __forceinline__ void update_kernel_body(const KernelArgs& a) {
     // work row: [Prob | Presolve]; the Presolve record is stored by update_phase itself
     Presolve* pre = reinterpret_cast<Presolve*>(a.work + (size_t)rb * WORK_LEN + PROB_LEN);
     if (a.elim && blockIdx.x == 0 && threadIdx.x == 0) a.fb[a.parity ^ 1] = 0;  // for the next update
-    const bool stance = update_phase<UPD_SUB, SOLVE>(a, rb, lane, wr, L.u[seg], L.prob[seg], pre, L.model);
+    const bool stance =
+        update_phase<UPD_SUB, false>(a, rb, rb, a.contacts[rb], lane, wr, L.u[seg], L.prob[seg], pre, L.model);
     const double2* src = reinterpret_cast<const double2*>(&L.prob[seg]);
     double2* dst = reinterpret_cast<double2*>(a.work + (size_t)rb * WORK_LEN);
-    if (wr && !(SOLVE && stance)) {
+    if (wr) {
         for (int k = lane; k < PROB_LEN / 2; k += UPD_SUB) dst[k] = src[k];
     }
     // QPs whose elimination did not happen go to the fallback list (rare: one atomic each): every
@@ -3421,8 +3934,44 @@ __device__ __forceinline__ void update_kernel_body(const KernelArgs& a) {
         }
     }
 }
-WBC_UPDATE_KERNEL_ATTR void wbc_update_kernel(KernelArgs a) { update_kernel_body<false>(a); }
-WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) { update_kernel_body<true>(a); }
+
+// The default wbc_step (and wbc_step_modes): one kernel per step, four QPs per wave, 16 lanes
+// each.  Segment seg of workgroup w is QP qp = 4 w + seg: its inputs and history are row qp, or,
+// under K mode hypotheses, state qp / K with contact mask mode_masks[qp % K] (the state's
+// dynamics are recomputed per hypothesis segment: four hypotheses of one state share a wave's
+// instruction stream, and nothing passes through HBM).  update_phase reduces and solves the QP in
+// place (§4.6, §4.8); a QP whose reduction is not usable (a near-singular stance leg) writes its
+// problem to work row qp (no slot factor: presolved = 0) and goes to the fallback list, which
+// wbc_solve_fallback_kernel solves with the general 24-variable method (launched with modes = 0:
+// the record carries the QP's own mask and masked bounds).
+WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) {
+    __shared__ UpdLds L;
+    const int seg = (int)threadIdx.x / UPD_SUB, lane = (int)threadIdx.x % UPD_SUB;
+    int qp = (int)blockIdx.x * UPD_RPW + seg;
+    const bool wr = qp < a.batch;  // a padding segment recomputes the last QP, writes nothing
+    if (!wr) qp = a.batch - 1;
+    const int K = a.modes;
+    const int row = K ? qp / K : qp;
+    const int kap = (K ? a.mode_masks[qp - row * K] : a.contacts[row]) & 15;
+    stage_to_lds<(int)(sizeof(wbc_model) / 8)>(reinterpret_cast<double*>(&L.model),
+                                                reinterpret_cast<const double*>(a.model), (int)threadIdx.x);
+    lds_sync();
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.fb[a.parity ^ 1] = 0;  // for the next step
+    const bool solved = update_phase<UPD_SUB, true>(a, row, qp, kap, lane, wr, L.u[seg], L.prob[seg], nullptr, L.model);
+    if (wr && !solved) {
+        const double2* src = reinterpret_cast<const double2*>(&L.prob[seg]);
+        double* wrow = a.work + (size_t)qp * WORK_LEN;
+        double2* dst = reinterpret_cast<double2*>(wrow);
+        for (int k = lane; k < PROB_LEN / 2; k += UPD_SUB) dst[k] = src[k];
+        if (lane == 0) {
+            Presolve* pre = reinterpret_cast<Presolve*>(wrow + PROB_LEN);
+            pre->presolved = 0.0;
+            pre->stance = 0.0;
+            const int idx = atomicAdd(&a.fb[a.parity], 1);
+            if (idx < a.fb_cap) a.fb[2 + idx] = qp;
+        }
+    }
+}
 
 // Four-contact QP whose equalities the update kernel eliminated (its Presolve::stance flag, in
 // the record registers): wbc_solve_stance_kernel's; every other QP is wbc_solve_kernel's.
@@ -3462,12 +4011,12 @@ __device__ void solve_general_qp(const KernelArgs& a, int rb, SolveLds& L) {
     PreRegs pf;
     pf.v0 = prow[lane_id()];
     pf.v1 = prow[64 + lane_id()];
-    const int kap_qp = qp_mask(a, rb, row);
+    const int kap_qp = a.elim ? qp_mask(a, rb, row) : 0;
     stage_to_lds<PROB_LEN / 2>(reinterpret_cast<double2*>(&L.prob),
                                reinterpret_cast<const double2*>(a.work + (size_t)row * WORK_LEN), lane_id());
     // the stance kernel's QP: checked after the problem copy is issued, so that a general QP's
     // loads all go out together (one HBM round trip)
-    if (a.elim && kap_qp == 15 && bcast(pf.v1, PRE_STANCE - 64) != 0.0) return;
+    if (a.elim && kap_qp == 15 && bcast(pf.v1, PRE_STANCE - 64) != 0.0) return;  // (kap_qp read only with elim)
     if (a.modes) {  // this hypothesis' contact mask on the unmasked bounds (update_phase)
         const int kap = a.mode_masks[rb - row * a.modes] & 15;
         const int lane = lane_id();
@@ -3521,7 +4070,6 @@ extern "C" hipError_t wbc_launch_step(const wbc::KernelArgs* a, hipStream_t st) 
     hipLaunchKernelGGL(wbc::wbc_step_kernel, dim3(a->batch), dim3(64), 0, st, *a);
     return hipGetLastError();
 }
-extern "C" int wbc_kernel_default_split() { return 1; }  // wbc_step: split kernels unless WBC_FUSED
 extern "C" int wbc_kernel_stance_elim() { return 1; }
 extern "C" hipError_t wbc_launch_update(const wbc::KernelArgs* a, hipStream_t st) {
     hipLaunchKernelGGL(wbc::wbc_update_kernel, dim3((a->batch + wbc::UPD_RPW - 1) / wbc::UPD_RPW), dim3(64), 0, st, *a);
@@ -3538,13 +4086,16 @@ extern "C" hipError_t wbc_launch_solve_stance(const wbc::KernelArgs* a, hipStrea
     hipLaunchKernelGGL(wbc::wbc_solve_fallback_kernel, dim3(16), dim3(64), 0, st, *a);
     return hipGetLastError();
 }
-// Stateless all-stance step in two launches: the update kernel solving the stance QPs inline,
-// then the fallback kernel for the QPs whose elimination failed.
+// The default step in two launches: the update kernel reducing and solving every QP inline, then
+// the fallback kernel for the QPs whose reduction was not usable (their records carry their own
+// mask and bounds: the general solve runs them with modes = 0 and no stance-kernel skip).
 extern "C" hipError_t wbc_launch_update_solve(const wbc::KernelArgs* a, hipStream_t st) {
-    if (!a->elim || a->stateful || a->modes) return hipErrorInvalidValue;
     hipLaunchKernelGGL(wbc::wbc_update_solve_kernel, dim3((a->batch + wbc::UPD_RPW - 1) / wbc::UPD_RPW), dim3(64), 0,
                        st, *a);
-    hipLaunchKernelGGL(wbc::wbc_solve_fallback_kernel, dim3(16), dim3(64), 0, st, *a);
+    wbc::KernelArgs f = *a;
+    f.modes = 0;
+    f.elim = 0;
+    hipLaunchKernelGGL(wbc::wbc_solve_fallback_kernel, dim3(16), dim3(64), 0, st, f);
     return hipGetLastError();
 }
 extern "C" hipError_t wbc_launch_reset(double* hist, const uint8_t* mask, int batch, hipStream_t st) {

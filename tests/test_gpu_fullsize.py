@@ -5,9 +5,14 @@ per pass); the smaller parity tests fit in one.  Each test runs the full batch o
 
   * compares a stratified sample of >= 512 rows against the C oracle (oracle/wbc_ref.c): rows
     spread over the whole batch, every pass boundary (multiples of 2048) and the last robot;
-    identical QP status and iteration counts, x* / tau at the tolerances of test_gpu_parity.py;
+    identical QP status (the literal 42 x 70 QP) and iteration counts (the oracle's REDUCED
+    method, the 12-variable form the default step solves), x* / tau at the tolerances of
+    test_gpu_parity.py;
   * re-runs the sampled rows as a small batch and requires bit-identical outputs (a robot's
-    result does not depend on where in the grid, or in which pass, it ran).
+    result does not depend on where in the grid, or in which pass, it ran).  One exception: a
+    mask-15 robot takes the four-contact stance form when its wave's four robots all have mask 15
+    and the general 12-variable form otherwise, so where resampling changes its
+    neighbours it agrees to rounding instead (status equal, iterations but for near-ties).
 """
 import numpy as np
 import pytest
@@ -44,8 +49,9 @@ def run(inp, modes=None):
 
 def check_vs_oracle(out, rows, inp_rows):
     o = R.run_batch(inp_rows)
+    red = R.run_batch(inp_rows, method=R.REDUCED)
     assert np.array_equal(out["status"][rows], o["status"])
-    same_it = out["iters"][rows] == o["iters"]
+    same_it = out["iters"][rows] == red["iters"]
     assert same_it.mean() >= 0.99, int((~same_it).sum())
     ok = o["status"] == 0
     for j in np.nonzero(ok)[0]:
@@ -64,8 +70,17 @@ def test_full_batch_sample_matches_oracle_and_small_batch(name, B, seed):
     sub = {k: np.ascontiguousarray(v[rows]) for k, v in inp.items()}
     check_vs_oracle(out, rows, sub)
     small = run(sub)
+    full15 = (inp["contacts"] == 15).reshape(-1, 4).all(1).repeat(4)[rows]
+    pad = (-len(rows)) % 4
+    sub15 = np.concatenate([sub["contacts"], np.full(pad, sub["contacts"][-1])]).reshape(-1, 4)
+    sub15 = (sub15 == 15).all(1).repeat(4)[:len(rows)]
+    same_form = full15 == sub15
     for k in KEYS:
-        assert np.array_equal(small[k], out[k][rows]), k
+        assert np.array_equal(small[k][same_form], out[k][rows][same_form]), k
+    d = ~same_form
+    assert np.array_equal(small["status"][d], out["status"][rows][d])
+    for k in ("tau", "x"):
+        assert np.max(np.abs(small[k][d] - out[k][rows][d]), initial=0.0) <= 1e-10 * (1 + np.max(np.abs(out[k]))), k
 
 
 def test_modes_full_shard_sample_matches_oracle_and_small_batch():

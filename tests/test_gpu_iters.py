@@ -1,11 +1,20 @@
 """GPU parity of the active-set bookkeeping: per-robot iteration counts and the nWSR cap.
 
 The reference solves with qpOASES under nWSR = 100 working-set changes (cpp:517) and stops the
-control loop when the solve fails (cpp:654-659).  The engine reports the same count per robot
-(`iters`, inequality working-set changes of the loop: adds and drops) and WBC_QP_MAX_ITER when it
-exceeds `max_wsr`.  The C oracle (oracle/wbc_ref.c, dense Goldfarb-Idnani on the 42 x 70 QP)
-counts the same quantity; both choose the most violated row by slack / |row of A| and take the
-same partial / full steps, so they visit the same working sets:
+control loop when the solve fails (cpp:654-659).  The engine reports a count per robot (`iters`,
+inequality working-set changes of its active-set loop: adds and drops) and WBC_QP_MAX_ITER when it
+exceeds `max_wsr`.  qpOASES' own count (a homotopy method) is not restated anywhere; the counts here
+are those of a Goldfarb-Idnani dual active set, on the QP form each engine path solves:
+
+  * the default wbc_step solves the exact 12-variable form (swing slacks and
+    stance equalities eliminated, so the slack rows never enter the working set); the C oracle's
+    REDUCED method (oracle/wbc_ref.c reduced_solve) solves the same form with the same rules;
+  * WBC_SPLIT (wbc_update + wbc_solve) solves the general 24-variable form, whose working sets are
+    those of the C oracle's LITERAL method (dense, on the 42 x 70 QP as assembled at cpp:466-515).
+
+Status, x and tau are the reference QP's whatever the form (checked against LITERAL).  Both pairs
+choose the most violated row by slack / |row of the reference's A| and take the same partial /
+full steps, so they visit the same working sets:
 
   * cold solves: identical status on every robot, identical `iters` on all but near-tie robots.
     Ties are real in this QP: a foot at zero force has all four friction faces active at one
@@ -20,7 +29,9 @@ import numpy as np
 import pytest
 
 import wbc_ref as R
-from quadrupedwholebodycontroller_amd import STATELESS, Engine, default_params, workloads
+from quadrupedwholebodycontroller_amd import SPLIT, STATELESS, Engine, default_params, workloads
+
+PATHS = {"default": (0, R.REDUCED), "split": (SPLIT, R.LITERAL)}  # engine flags, oracle method
 
 pytestmark = pytest.mark.gpu
 
@@ -36,7 +47,7 @@ def stress_inputs(B, seed):
     return inp
 
 
-def engine_cold(inp, **ov):
+def engine_cold(inp, flags=0, **ov):
     B = inp["base_pose"].shape[0]
     p = default_params()
     for k, v in ov.items():
@@ -44,7 +55,7 @@ def engine_cold(inp, **ov):
     e = Engine(B, params=p)
     e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
     e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
-    e.step(STATELESS)
+    e.step(STATELESS | flags)
     out = e.outputs()
     e.close()
     return out
@@ -58,29 +69,37 @@ CASES = {  # name: (inputs, params, min fraction of robots with identical iterat
 }
 
 
+@pytest.mark.parametrize("path", sorted(PATHS))
 @pytest.mark.parametrize("case", sorted(CASES))
-def test_cold_iterations_match_oracle(case):
+def test_cold_iterations_match_oracle(case, path):
     gen, ov, frac = CASES[case]
+    flags, method = PATHS[path]
     inp = gen()
-    g, o = engine_cold(inp, **ov), R.run_batch(inp, **ov)
-    assert np.array_equal(g["status"], o["status"]), case
+    g, o = engine_cold(inp, flags, **ov), R.run_batch(inp, method=method, **ov)
+    lit = o if method == R.LITERAL else R.run_batch(inp, **ov)
+    assert np.array_equal(g["status"], o["status"]) and np.array_equal(g["status"], lit["status"]), case
     same = g["iters"] == o["iters"]
     assert same.mean() >= frac, (case, int((~same).sum()), np.unique(g["iters"] - o["iters"], return_counts=True))
+    ok = lit["status"] == 0
+    assert np.max(np.abs(g["tau"][ok] - lit["tau"][ok])) <= 1e-7 * (1 + np.max(np.abs(lit["tau"][ok])))
 
 
-CAPS = {"stance": [1, 2, 3], "rl_random": [4, 8, 12], "stress20": [10, 20, 30]}
+CAPS = {"stance": [1, 2, 3], "rl_random": [2, 4, 8], "stress20": [5, 10, 15]}
+CAPS_SPLIT = {"rl_random": [4, 8, 12], "stress20": [10, 20, 30]}
 
 
-@pytest.mark.parametrize("case,max_wsr", [(c, m) for c, ms in CAPS.items() for m in ms])
-def test_max_iter_status_matches_oracle(case, max_wsr):
+@pytest.mark.parametrize("case,max_wsr,path", [(c, m, "default") for c, ms in CAPS.items() for m in ms] +
+                         [(c, m, "split") for c, ms in CAPS_SPLIT.items() for m in ms])
+def test_max_iter_status_matches_oracle(case, max_wsr, path):
     """nWSR lowered so that the cap splits the batch: WBC_QP_MAX_ITER on the same robots as the
-    oracle's MAX_ITER; the others solve to the same torques."""
+    oracle's MAX_ITER (same QP form); the others solve to the same torques."""
+    flags, method = PATHS[path]
     if case == "stance":
         inp, ov = workloads.stance_cold(512, 5), {}
     else:
         gen, ov, _ = CASES[case]
         inp = {k: v[:512] for k, v in gen().items()}
-    g, o = engine_cold(inp, max_wsr=max_wsr, **ov), R.run_batch(inp, max_wsr=max_wsr, **ov)
+    g, o = engine_cold(inp, flags, max_wsr=max_wsr, **ov), R.run_batch(inp, method=method, max_wsr=max_wsr, **ov)
     hit = o["status"] == 1
     assert hit.any() and (~hit).any(), "cap must split the batch"
     mism = np.nonzero(g["status"] != o["status"])[0]
@@ -97,22 +116,26 @@ def _trot(B, steps, seed):
     return list(workloads.trot_sequence(B, steps=steps, seed=seed))
 
 
+@pytest.mark.parametrize("path", sorted(PATHS))
 @pytest.mark.parametrize("max_wsr", [100, 2])
-def test_hotstart_iterations_match_oracle(max_wsr):
+def test_hotstart_iterations_match_oracle(max_wsr, path):
     """Stateful trot: the engine hotstarts from the previous working set, the oracle's Robot does
-    the same (init on cycle 1, hotstart afterwards); status and iterations agree on every step."""
+    the same (init on cycle 1, hotstart afterwards; the 12-variable form keeps the rows that still
+    exist across a contact change, the general form only under an unchanged mask); status and
+    iterations agree on every step."""
+    flags, method = PATHS[path]
     B, steps = 48, 120
     seq = _trot(B, steps, seed=29)
     p = default_params()
     p.max_wsr = max_wsr
     p.max_torque = 40.0  # torque rows bind, so warm sets carry inequalities
     e = Engine(B, params=p)
-    robots = [R.Robot(hotstart=True, max_wsr=max_wsr, max_torque=40.0) for _ in range(B)]
+    robots = [R.Robot(hotstart=True, method=method, max_wsr=max_wsr, max_torque=40.0) for _ in range(B)]
     n_it = n_mism = n_cap = 0
     for t, inp in enumerate(seq):
         e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
         e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
-        e.step(0)
+        e.step(flags)
         g = e.outputs()
         for b in range(B):
             o = robots[b].step(inp["base_pose"][b], inp["nu"][b], inp["qj"][b], inp["ref"][b],

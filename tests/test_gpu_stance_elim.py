@@ -169,6 +169,6 @@ def test_all_stance_modes_equal_per_row():
     got = e.outputs()
     e.close()
     rep = {k: np.repeat(v, K, axis=0) for k, v in inp.items()}
-    want = run(rep, split=True)
+    want = run(rep)
     for k in KEYS:
         assert np.array_equal(got[k], want[k]), k
