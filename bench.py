@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Benchmark: batched ANYmal WBC QP solves/s on MI355X (BASELINE.json metric).
 
-One step = one wbc_step over the rank's batch (dynamics + centroidal assembly + QP + torques:
-the update kernel then the solve kernel, the build's default form), plus for N > 1 the RCCL
-all-gather of the torque block.  Inputs are
+One step = one wbc_step over the rank's batch (dynamics + centroidal assembly + QP + torques: one
+kernel, wbc_update_solve_kernel, four QPs per wave, each reduced exactly to 12 variables and
+solved in place; plus the near-empty fallback launch), plus for N > 1 the RCCL all-gather of the
+torque block.  Inputs are
 resident in HBM before the timed region.  Default workload: configs[1] of BASELINE.json,
 B = 4096 four-contact stance states, cold solves, per GPU (weak scaling).
 
@@ -35,7 +36,8 @@ CONFIGS = {
                             desc="BASELINE configs[3] per-GPU shard: randomized q/qd, 16 contact masks, cold"),
     "modes16_b16384": dict(gen="modes16", batch=16384, seed=4, modes=16, scaling="weak",
                            desc="BASELINE configs[4] per-GPU shard: 1024 states x all 16 contact masks, cold; "
-                                "wbc_step_modes (dynamics + assembly once per state, 16 QPs per state)"),
+                                "wbc_step_modes (one 16-lane segment per hypothesis, the state's inputs shared "
+                                "through L2)"),
     # the two multi-GPU configurations at their global sizes (strong scaling: total work fixed)
     "rl_random_b65536": dict(gen="rl_random", batch=65536, seed=3, scaling="strong",
                              desc="BASELINE configs[3]: global B=65536 randomized q/qd (16 contact masks, cold), "
@@ -163,6 +165,21 @@ def committed_traffic(workload, batch):
     return {}, None
 
 
+def step_flops(S, iters):
+    """SURVEY 8(d) algorithmic flops of one step: F_dyn + F_asm per state (mode hypotheses share
+    their state's dynamics), F_fact + F_tau + k F_iter per QP with k = iters[] (the working-set
+    changes of the form the engine solved)."""
+    iters = np.asarray(iters, np.int64)
+    return float(S * (F_DYN + F_ASM) + np.sum(F_FACT + F_TAU + F_ITER * iters))
+
+
+def roofline_of(flops, kernel_ms, traffic=None, traffic_src=None):
+    tf = flops / (kernel_ms * 1e-3) / 1e12
+    return {"bound": "fp64_valu", "achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": tf / FP64_PEAK_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
+            "kernel": "wbc_update_solve_kernel", "kernel_ms": kernel_ms, "flops_per_launch": flops}
+
+
 def make_engine(cfg, B, seed, device, stream):
     """Engine for a bench config on `stream`, inputs loaded; returns (engine, step flags fn, inputs).
     Mode-hypothesis configs hold B / K states and step with wbc_step_modes."""
@@ -193,15 +210,18 @@ def bench_trot(torch, stream, device, STATELESS, B=4096, T=400, seed=2):
     e = Engine(B, device=device)
     e.set_stream(stream.cuda_stream)
 
-    def run():
+    def run(iters_out=None):
         e.reset()
         for t in range(T):
             e.bind_device_inputs(dev["base_pose"][t].data_ptr(), dev["nu"][t].data_ptr(), dev["qj"][t].data_ptr(),
                                  dev["ref"][t].data_ptr(), dev["contacts"][t].data_ptr(),
                                  dev["switching"][t].data_ptr())
             e.step(NO_X)  # stateful
+            if iters_out is not None:
+                iters_out.append(e.outputs()["iters"].astype(np.int64))
 
-    run()  # warm-up pass
+    its = []
+    run(its)  # warm-up pass; its iteration counts (the same inputs every pass) for the flop count
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
@@ -213,9 +233,13 @@ def bench_trot(torch, stream, device, STATELESS, B=4096, T=400, seed=2):
     ms = ev0.elapsed_time(ev1)
     o = e.outputs()
     e.close()
+    its = np.stack(its)
+    rl = roofline_of(step_flops(B * T, its) / T, ms / T)
+    rl["note"] = "per step (one wbc_update_solve_kernel launch + the fallback launch): flops of the 400-step " \
+                 "sequence / 400 over the sequence's HIP-event time / 400"
     return dict(batch=B, steps=T, ms_total=ms, ms_per_step=ms / T, solves_per_s=B * T / (ms * 1e-3),
                 wall_solves_per_s=B * T / wall, status_counts_last=np.bincount(o["status"], minlength=4).tolist(),
-                mean_iters_last=float(o["iters"].mean()),
+                mean_iters_last=float(o["iters"].mean()), mean_iters=float(its.mean()), roofline=rl,
                 desc="BASELINE configs[2]: trot, alternating 2-contact modes, stateful history, inputs staged in HBM")
 
 
@@ -304,7 +328,7 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    from quadrupedwholebodycontroller_amd import FUSED, NO_X, STATELESS, Engine
+    from quadrupedwholebodycontroller_amd import FUSED, NO_X, SPLIT, STATELESS, Engine
     from quadrupedwholebodycontroller_amd.sharding import (StepOutputs, gather_step_outputs, shard_capacity,
                                                            unpack_gathered)
 
@@ -400,52 +424,25 @@ def main():
         torch.cuda.synchronize()
         return ev0.elapsed_time(ev1) / args.steps
 
-    # A step is the update kernel (dynamics + assembly, four robots per wave) then the solve: for an
-    # all-stance batch (the engine's choice) the stance solve kernel and the fallback
-    # kernel, otherwise the general solve kernel.  Each part is timed alone on the launch stream;
-    # the dominant one carries the roofline.
-    # A stateless all-stance wbc_step (the headline) is one kernel that also solves the stance QPs
-    # (wbc_update_solve_kernel) plus the elimination-fallback kernel, near empty
-    # (no near-singular legs in the bench states): the step's time is that kernel's, with the
-    # empty launch behind it (rocprofv3 in profiles/ separates the two).
-    elim = (not K) and bool(np.all((inp["contacts"] & 15) == 15))
-    inline = elim
-    solve_name = "wbc_solve_stance_kernel" if elim else "wbc_solve_kernel"
+    # A step is one kernel (wbc_update_solve_kernel: dynamics, the QP reduced to 12 variables and
+    # solved in the same wave, torques) plus the elimination-fallback kernel, near empty (no
+    # near-singular legs in the bench states): the step's time is that kernel's, with the empty launch
+    # behind it (rocprofv3 in profiles/ separates the two).  It owns all of SURVEY 8(d)'s flops.
     step_ms = timed(lambda: step(STEP_FLAGS))
     out = e.outputs()
     iters = out["iters"].astype(np.int64)
     status = out["status"]
-    if K:  # wbc_step_modes launches the pair together: the update of the S states is timed on an
-        # S-robot engine holding the same inputs, the solve kernel is the rest of the step
-        e_k = Engine(S, device=local_rank)
-        e_k.set_stream(stream.cuda_stream)
-        e_k.set_state(inp["base_pose"], inp["nu"], inp["qj"])
-        e_k.set_reference(inp["ref"], inp["contacts"], inp["switching"])
-        upd_ms = timed(lambda: e_k.update(STEP_FLAGS))
-        solve_ms = step_ms - upd_ms
-        e_k.close()
-    elif not inline:
-        upd_ms = timed(lambda: e.update(STEP_FLAGS))
-        solve_ms = timed(lambda: e.solve(STEP_FLAGS))  # re-solves the assembled problem (stateless)
-    kernels = {"wbc_update_solve_kernel": step_ms} if inline else {"wbc_update_kernel": upd_ms, solve_name: solve_ms}
-    dom = max(kernels, key=kernels.get)
-    dom_ms = kernels[dom]
-    # flops owned by each kernel: dynamics + assembly in the update, factorisation + active-set
-    # iterations + torques in the solve (SURVEY 8d's dense-problem counts, whatever form computes them)
-    # An all-stance step factors the QP in the update kernel (the equality elimination and the
-    # force-space Cholesky), so F_fact is the update kernel's there; otherwise the
-    # solve kernel's equality block is the counterpart of the reference's initial factorisation.
-    f_fact_upd = F_FACT if elim else 0
-    flops_k = {"wbc_update_kernel": float(S * (F_DYN + F_ASM + f_fact_upd)),
-               solve_name: float(np.sum(F_TAU + (F_FACT - f_fact_upd) + F_ITER * iters))}
-    flops_k["wbc_update_solve_kernel"] = flops_k["wbc_update_kernel"] + flops_k[solve_name]
-    tf_dom = flops_k[dom] / (dom_ms * 1e-3) / 1e12
+    kernels = {"wbc_update_solve_kernel": step_ms}
+    dom, dom_ms = "wbc_update_solve_kernel", step_ms
+    flops_step = step_flops(S, iters)
+    tf_dom = flops_step / (dom_ms * 1e-3) / 1e12
     bytes_step = S * BYTES_IN + B * BYTES_OUT
     hbm_gbs = bytes_step / (step_ms * 1e-3) / 1e9
 
     breakdown = None
-    if args.breakdown and not K:  # the fused single-kernel form of the same step, for comparison
-        breakdown = dict(fused_step_ms=timed(lambda: e.step(STEP_FLAGS | FUSED)), split_step_ms=step_ms)
+    if args.breakdown and not K:  # the general method's forms of the same step, for comparison
+        breakdown = dict(step_ms=step_ms, fused64_step_ms=timed(lambda: e.step(STEP_FLAGS | FUSED)),
+                         split_step_ms=timed(lambda: e.step(STEP_FLAGS | SPLIT)))
 
     extra = {}
     if args.extra and rank == 0:
@@ -460,16 +457,17 @@ def main():
             ms2 = timed(lambda: step2(STEP_FLAGS))
             o2 = e2.outputs()
             tr2, tr2_src = committed_traffic(name, B2)
+            S2 = B2 // (c2.get("modes") or 1)
             extra[name] = dict(batch=B2, ms_per_step=ms2, solves_per_s=B2 / (ms2 * 1e-3),
                                status_counts=np.bincount(o2["status"], minlength=4).tolist(),
                                mean_iters=float(o2["iters"].mean()), desc=c2["desc"],
+                               roofline=roofline_of(step_flops(S2, o2["iters"]), ms2, tr2.get("step"), tr2_src),
                                traffic_per_step=tr2.get("step"), traffic_source=tr2_src,
-                               algorithmic_bytes_per_step=float((B2 // (c2.get("modes") or 1)) * BYTES_IN +
-                                                                B2 * BYTES_OUT))
+                               algorithmic_bytes_per_step=float(S2 * BYTES_IN + B2 * BYTES_OUT))
             e2.close()
 
     traffic, traffic_src = committed_traffic(args.config, B)
-    if elim and traffic:  # the fallback kernel (near empty) is part of the stance step
+    if traffic:  # the fallback kernel (near empty) is part of the step
         traffic = dict(traffic)
         traffic["wbc_update_solve_kernel"] = (traffic.get("wbc_update_solve_kernel") or 0.0) + \
             (traffic.get("wbc_solve_fallback_kernel") or 0.0)
@@ -497,12 +495,12 @@ def main():
                      "frac": tf_dom / FP64_PEAK_TFLOPS, "traffic": traffic.get(dom),
                      "traffic_source": traffic_src, "kernel": dom, "kernel_ms": dom_ms,
                      "kernels_ms": kernels, "step_kernels_ms": step_ms,
-                     "note": "dominant kernel; fp64 VALU roof (no MFMA on this path; gfx950 fp64 vector peak); "
-                             "algorithmic flops of SURVEY 8(d) owned by this kernel: update = F_dyn + F_asm, solve = "
-                             "F_fact + F_tau + k F_iter, k = iters[] per robot; a stateless all-stance step is one "
-                             "kernel owning all of them (wbc_update_solve_kernel; its kernel_ms is the step's, with "
-                             "the empty fallback launch); latency/issue-bound small dense linear algebra",
-                     "flops_per_launch": flops_k[dom]},
+                     "note": "the step's one kernel (wbc_update_solve_kernel; its kernel_ms is the step's, with "
+                             "the near-empty fallback launch); fp64 VALU roof (no MFMA on this path; gfx950 fp64 "
+                             "vector peak); SURVEY 8(d) algorithmic flops: F_dyn + F_asm per state, F_fact + F_tau + "
+                             "k F_iter per QP, k = iters[] (working-set changes of the 12-variable form the engine "
+                             "solves); latency/issue-bound small dense linear algebra",
+                     "flops_per_launch": flops_step},
         "roofline_hbm": {"bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": hbm_gbs / HBM_PEAK_GBS, "bytes_per_solve": bytes_step / B,
                          "traffic": sum(traffic.get(k, 0) for k in kernels) if traffic else None,

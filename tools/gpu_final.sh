@@ -5,7 +5,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 TAG=${TAG:-final}
-ROUND=${ROUND:-r02}
+ROUND=${ROUND:-r03}
 O=gpurun_out/$TAG
 mkdir -p $O profiles/$ROUND
 step() { local name=$1 t=$2; shift 2; echo "== $name $(date +%T)"; timeout -k 10 $t "$@" > $O/$name.log 2>&1; local rc=$?; echo "== $name rc=$rc"; if [ $rc -ne 0 ]; then tail -30 $O/$name.log; exit $rc; fi; }
@@ -18,7 +18,14 @@ for cb in stance_cold_b4096:4096 rl_random_b8192:8192 modes16_b16384:16384; do
   cp $O/pmc_$c.json profiles/$ROUND/pmc_$c.json  # read by bench.py below
 done
 step bench 300 python bench.py --steps 50 --warmup 5
-step bench_extra 300 python bench.py --steps 20 --warmup 3 --extra --no-cpu-baseline
+step bench_extra 300 python bench.py --steps 20 --warmup 3 --extra --breakdown --no-cpu-baseline
 step prof 300 rocprofv3 --kernel-trace --stats -d $O/prof -o prof --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline
+for cb in rl_random_b8192 modes16_b16384; do
+  step prof_$cb 300 rocprofv3 --kernel-trace --stats -d $O/prof_$cb -o prof --output-format csv -- python3 bench.py --config $cb --steps 50 --warmup 5 --no-cpu-baseline
+done
+step b1_fused 120 quadrupedwholebodycontroller_amd/wbc_control_loop stance 3000 0 fused
+step b1_default 120 quadrupedwholebodycontroller_amd/wbc_control_loop stance 3000 0 default
+step ust_stance 120 env WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_istamps.so python tools/ust16.py stance_cold 4096
+step ust_rl 120 env WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_istamps.so python tools/ust16.py rl_random 8192
 tail -1 $O/bench.log
 echo final done
