@@ -600,6 +600,54 @@ __device__ bool factor12(double (&hrow)[12], double gsv, int lane, double (&L)[1
     return chol_ok;
 }
 
+// The same factorisation for the inline solve of the general 12-variable form (§4.8), without the
+// LDS round trips of factor12: the Cholesky as there (row i in lane i), then lane j forms column j of
+// M = L^-1 by forward substitution with L's entries broadcast from their rows' lanes (DPP); column j
+// of M is row j of J0 = L^-T, written straight into the J mirror (`Jm`, 12 x 12 row-major, J rows as
+// solve16 keeps them); x0 = -H^-1 g = -J0 (J0^T g) (the mirror's columns, then the lane's own row).
+// Returns false when H is not positive definite.
+__device__ bool factor12_rows(double (&hrow)[12], double gsv, int lane, double* Jm, double* xs) {
+    bool chol_ok = true;
+    double ildv = 1.0;  // lane k: 1 / L_kk
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        const double dkk = seg_bcast<16>(hrow[k], k);
+        chol_ok &= dkk > 0.0;
+        const double il = fast_rsq(fmax(dkk, 1e-300));
+        const double lkk = dkk * il;
+        if (lane == k) ildv = il;
+        hrow[k] = (lane == k) ? lkk : hrow[k] * il;
+#pragma unroll
+        for (int j = k + 1; j < 12; ++j) hrow[j] = fma(-hrow[k], seg_bcast<16>(hrow[k], j), hrow[j]);
+    }
+    // lane j: m = column j of M (m[i] = 0 for i < j); L[i][k] = hrow[k] of lane i
+    double m[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+        double a4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k = 0; k < i; ++k) a4[k & 3] = fma(seg_bcast<16>(hrow[k], i), m[k], a4[k & 3]);
+        m[i] = (((lane == i) ? 1.0 : 0.0) - ((a4[0] + a4[1]) + (a4[2] + a4[3]))) * seg_bcast<16>(ildv, i);
+    }
+    if (lane < 12) {
+#pragma unroll
+        for (int j = 0; j < 12; j += 2) *reinterpret_cast<double2*>(&Jm[lane * 12 + j]) = make_double2(m[j], m[j + 1]);
+    }
+    lds_sync();
+    // z = J0^T g (lane i: column i of the mirror . g), x0_l = -(J0 row l) . z
+    const int i = lane < 12 ? lane : 0;
+    double z4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < 12; ++k) z4[k & 3] = fma(Jm[k * 12 + i], seg_bcast<16>(gsv, k), z4[k & 3]);
+    const double zi = (z4[0] + z4[1]) + (z4[2] + z4[3]);
+    double x4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < 12; ++k) x4[k & 3] = fma(m[k], seg_bcast<16>(zi, k), x4[k & 3]);
+    if (lane < 12) xs[lane] = -((x4[0] + x4[1]) + (x4[2] + x4[3]));
+    lds_sync();
+    return chol_ok;
+}
+
 // Slot factorisation of the general solve: H_s, its factor, M = L^-1 and x0's slot part.  Runs
 // at the end of the update (four robots per wave in the update kernel) or, under mode
 // hypotheses, in the solve.  Returns false when H_s is not positive definite.
@@ -1344,6 +1392,7 @@ __device__ bool reduce_general([[maybe_unused]] const KernelArgs& ka, [[maybe_un
         }
     }
     double blk[3] = {0.0, 0.0, 0.0}, gown = 0.0;
+    double Ci[6];  // C_a: P_a = E_a^T (stance slot) or o_a (swing slot), broadcast to the segment in R6
     {
         // o_a = w sum_r J_l[r][k] v_(l,r) (swing slot a = (l, k)); stance slot: C_a = P_a = E_a^T
         double oa[6] = {0, 0, 0, 0, 0, 0};
@@ -1356,12 +1405,8 @@ __device__ bool reduce_general([[maybe_unused]] const KernelArgs& ka, [[maybe_un
             for (int kj = 0; kj < 3; ++kj) blk[kj] = fma(jrk, s.Jf[l][3 * r + kj], blk[kj]);
             gown = fma(jrk, V.rho0[3 * l + r], gown);
         }
-        if (lane < 12) {
 #pragma unroll
-            for (int c = 0; c < 6; c += 2)
-                *reinterpret_cast<double2*>(&V.Ct[i * 6 + c]) =
-                    make_double2(sti ? Ei[c] : wsw * oa[c], sti ? Ei[c + 1] : wsw * oa[c + 1]);
-        }
+        for (int c = 0; c < 6; ++c) Ci[c] = sti ? Ei[c] : wsw * oa[c];
     }
     lds_sync();
     UST(ka, rb, 21);
@@ -1383,30 +1428,32 @@ __device__ bool reduce_general([[maybe_unused]] const KernelArgs& ka, [[maybe_un
         // beta_a = V B_a + o_a
 #pragma unroll
         for (int c = 0; c < 6; ++c) {
-            double t = sti ? 0.0 : V.Ct[i * 6 + c];
+            double t = sti ? 0.0 : Ci[c];
 #pragma unroll
             for (int b = 0; b < 6; ++b) t = fma(R.Q[c][b], Bi[b], t);
             be[c] = t;
         }
 #pragma unroll
+        // B_j and C_j from lane j of the segment (DPP broadcasts: no LDS round trip per column,
+        // which the register-bound schedule issued and waited for one at a time)
         for (int j = 0; j < 12; ++j) {
             const bool stj = (kap >> (j / 3)) & 1;
             double bj[6], cj[6];
 #pragma unroll
-            for (int c = 0; c < 6; c += 2) {
-                const double2 b2 = *reinterpret_cast<const double2*>(&V.Bt[j * 6 + c]);
-                const double2 c2 = *reinterpret_cast<const double2*>(&V.Ct[j * 6 + c]);
-                bj[c] = b2.x; bj[c + 1] = b2.y; cj[c] = c2.x; cj[c + 1] = c2.y;
+            for (int c = 0; c < 6; ++c) {
+                bj[c] = seg_bcast<16>(Bi[c], j);
+                cj[c] = seg_bcast<16>(Ci[c], j);
             }
             double h = (i == j) ? 1.0 : 0.0;
             if (!sti && j / 3 == l) h = fma(wsw, sel3d(j % 3, blk[0], blk[1], blk[2]), h);
-            double t1 = 0.0, t2 = 0.0;
+            double t1 = 0.0, ta = 0.0, tb = 0.0;  // both dots, one select (not one per component)
 #pragma unroll
             for (int c = 0; c < 6; ++c) {
                 t1 = fma(be[c], bj[c], t1);
-                t2 = fma(stj ? al[c] : Bi[c], cj[c], t2);
+                ta = fma(al[c], cj[c], ta);
+                tb = fma(Bi[c], cj[c], tb);
             }
-            hrow[j] = h + t1 + t2;
+            hrow[j] = h + t1 + (stj ? ta : tb);
         }
         double gam = 0.0;
 #pragma unroll
@@ -1422,7 +1469,7 @@ __device__ bool reduce_general([[maybe_unused]] const KernelArgs& ka, [[maybe_un
     UST(ka, rb, 22);
     // R7: H = L L^T, M = L^-1, x0 = -H^-1 g (ps.L, ps.xs: over W .. Si, all read by now)
     lds_sync();
-    ok = factor12<16>(hrow, gsv, lane, s.ps.L, s.ps.ild, s.ps.xs);
+    ok = factor12_rows(hrow, gsv, lane, &s.ps.L[0][0], s.ps.xs);
     if (!ok) return false;
     // R8: torque map row r = i, t0_r, the row's reference-space norm; then Nt over Jbj
     {
@@ -2597,7 +2644,7 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
         bool vac = false;
         if (reduce_general(a, rb, P, pr, lane, kap, s, V, vac)) {
             UST(a, rb, 11);
-            solve16<false, true>(a, rb, qp, lane, wr, P, s, V, kap, vac ? WBC_QP_INFEASIBLE : WBC_QP_OK);
+            solve16<true, true>(a, rb, qp, lane, wr, P, s, V, kap, vac ? WBC_QP_INFEASIBLE : WBC_QP_OK);
             return true;
         }
         return false;
