@@ -1315,11 +1315,12 @@ __device__ bool reduce_general([[maybe_unused]] const KernelArgs& ka, [[maybe_un
     if (!ok) return false;
     // R4: Y_i = W_i S6^-1, q0_i = w_i + Y_i z6 (zero on swing rows); per lane: B_i, v_i, rho0_i
     double Bi[6], Ei[6];  // column i of B, E_i^T = [e_k; row k of -S(d_l)]
+    double yi[6], q;      // Y_i, q0_i (kept for the torque map, R8)
     {
-        double wrow[6], yi[6];
+        double wrow[6];
 #pragma unroll
         for (int c = 0; c < 6; ++c) wrow[c] = R.W[i][c];
-        double q = R.w[i];
+        q = R.w[i];
 #pragma unroll
         for (int c = 0; c < 6; ++c) {
             double a4[2] = {0.0, 0.0};
@@ -1475,6 +1476,7 @@ __device__ bool reduce_general([[maybe_unused]] const KernelArgs& ka, [[maybe_un
     {
         const int r = i;
         double my[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, t4[2] = {0.0, 0.0}, s2 = 0.0, mrow[12];
+        // Y_kk, q0_kk and B_j from their lanes (DPP broadcasts, as the H rows)
 #pragma unroll
         for (int kk = 0; kk < 12; ++kk) {
             const double mk = P.Mbj[r * 12 + kk];
@@ -1482,8 +1484,8 @@ __device__ bool reduce_general([[maybe_unused]] const KernelArgs& ka, [[maybe_un
             const double jc = stk ? P.Jbj[kk * 12 + r] : 0.0;
             mrow[kk] = stk ? jc : -mk;  // the slot's own term of Nt[r][kk]
 #pragma unroll
-            for (int c = 0; c < 6; ++c) my[c] = fma(mk, R.Y[kk][c], my[c]);
-            t4[kk & 1] = fma(mk, R.q0[kk], t4[kk & 1]);
+            for (int c = 0; c < 6; ++c) my[c] = fma(mk, seg_bcast<16>(yi[c], kk), my[c]);
+            t4[kk & 1] = fma(mk, seg_bcast<16>(q, kk), t4[kk & 1]);
             s2 = fma(mk, mk, fma(jc, jc, s2));
         }
         double nt[12];
@@ -1491,7 +1493,7 @@ __device__ bool reduce_general([[maybe_unused]] const KernelArgs& ka, [[maybe_un
         for (int j = 0; j < 12; ++j) {
             double t = mrow[j];
 #pragma unroll
-            for (int c = 0; c < 6; ++c) t = fma(-my[c], V.Bt[j * 6 + c], t);
+            for (int c = 0; c < 6; ++c) t = fma(-my[c], seg_bcast<16>(Bi[c], j), t);
             nt[j] = t;
         }
         const double t0v = P.bbj[r] + (t4[0] + t4[1]);
@@ -1625,18 +1627,15 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
     bool done = (status != WBC_QP_OK);
     const int max_wsr = pr.max_wsr;
 
-    // d = J^T n (lane j: column j of the mirror . n), broadcast to every lane; d2 = rows >= pos;
+    // d = J^T n (lane j: dj = column j of the mirror . n), broadcast to every lane; d2 = rows >= pos;
     // r = R^-1 d (lane l < q), zn = |d2|^2, z = J2 d2 (lane k: z_k), dq = d[pos], jq = J[l][pos]
-    auto direction = [&](const double* jc, const double* np, int pos, double* d2, double& rk, double& zn, double& zk,
-                         double& dq, double& jq) {
-        double dj;
-        {
-            double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    auto dot_col = [&](const double* jc, const double* np) {
+        double acc[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int k = 0; k < N; ++k) acc[k & 3] += jc[k] * np[k];
-            dj = (l < N) ? (acc[0] + acc[1]) + (acc[2] + acc[3]) : 0.0;
-        }
-        lds_sync();
+        for (int k = 0; k < N; ++k) acc[k & 3] += jc[k] * np[k];
+        return (l < N) ? (acc[0] + acc[1]) + (acc[2] + acc[3]) : 0.0;
+    };
+    auto direction = [&](double dj, int pos, double* d2, double& rk, double& zn, double& zk, double& dq, double& jq) {
         double d[N];
 #pragma unroll
         for (int k = 0; k < N; ++k) d[k] = seg_bcast<16>(dj, k);
@@ -1723,7 +1722,7 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
 #pragma unroll
                     for (int k = 0; k < N; ++k) { np[k] = V.col[k]; nn = fma(np[k], np[k], nn); }
                     double d2[N], rk, zn, zk, dq, jq;
-                    direction(jc, np, pos, d2, rk, zn, zk, dq, jq);
+                    direction(dot_col(jc, np), pos, d2, rk, zn, zk, dq, jq);
                     if (!(zn > 1e-26 * fmax(1.0, nn))) { fail = true; break; }  // dependent: reject
                     householder_add(pos, d2, rk, zn, zk, dq, jq);
                     if (l == pos) act = p;
@@ -1787,6 +1786,7 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
     };
     if (!done) select();
 
+    IST_DECL;
     while (__any(!done)) {
         // column i of J from the mirror, issued first so that its LDS latency is off the chain
         double jc[N];
@@ -1795,18 +1795,30 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
         if (!done && ++iters > max_wsr) { status = WBC_QP_MAX_ITER; iters = max_wsr; done = true; }
         if (!done) {
             const int pos = q, ol = pstar & 15, js = pstar >> 4;
-            if (l == ol) {  // the chosen row's normal and slack, from its lane
+            // dj = column j of J . n for the chosen row, from the row id alone (no exchange of its
+            // normal through the owner lane): a torque row is +-row jt of Nt (LDS, one address per
+            // segment), a friction face -D[rp] = (f0, f1, mu) on leg lg's slot; the slack from the
+            // owner lane
+            double dj;
+            {
+                const bool frc = pstar < 16;
+                const int tq = pstar - 16, jt = frc ? 0 : (tq >> 1), rp = pstar & 3, lg = (pstar >> 2) & 3;
+                double a4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-                for (int k = 0; k < N; ++k) V.col[k] = sel3d(js, n0[k], n1[k], n2[k]);
-                V.col[12] = sel3d(js, sp0, sp1, sp2);
+                for (int k = 0; k < N; ++k) a4[k & 3] = fma(jc[k], V.Nt[jt * 12 + k], a4[k & 3]);
+                const double dt = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+                const double f0 = (rp == 0) ? -1.0 : (rp == 1 ? 1.0 : 0.0), f1 = (rp == 2) ? -1.0 : (rp == 3 ? 1.0 : 0.0);
+                double gl[4];
+#pragma unroll
+                for (int L = 0; L < 4; ++L) gl[L] = fma(jc[3 * L], f0, fma(jc[3 * L + 1], f1, jc[3 * L + 2] * pr.friction));
+                const double df = sel4d(lg, gl[0], gl[1], gl[2], gl[3]);
+                dj = (l < N) ? (frc ? df : ((tq & 1) ? dt : -dt)) : 0.0;
             }
-            lds_sync();
-            double np[N];
-#pragma unroll
-            for (int k = 0; k < N; ++k) np[k] = V.col[k];
-            const double sps = V.col[12];
+            const double sps = seg_shfl(sel3d(js, sp0, sp1, sp2), ol);
+            IST(0);  // the chosen row's normal
             double d2[N], rk, zn, zk, dq, jq;
-            direction(jc, np, pos, d2, rk, zn, zk, dq, jq);
+            direction(dj, pos, d2, rk, zn, zk, dq, jq);
+            IST(1);  // d = J^T n, R^-1 d, z
             // slack rates n . z of the lane's rows (z_m broadcast from lane m)
             double cz0, cz1, cz2;
             {
@@ -1822,6 +1834,7 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
                 cz1 = (z1[0] + z1[1]) + (z1[2] + z1[3]);
                 cz2 = (z2[0] + z2[1]) + (z2[2] + z2[3]);
             }
+            IST(2);  // slack rates
             // step: t1 (drop an active slot) or t2 (the new row becomes active)
             const double vt = (l < q && rk > 1e-14) ? u * fast_rcp(rk) : 1e300;
             // the exact minimum (fmin returns one of its inputs), then its lowest lane from a
@@ -1831,6 +1844,7 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
             const int l1 = __builtin_ctzll((__ballot(vt == t1) >> ((int)threadIdx.x & 48)) & 0xFFFFull);
             const double t2 = (zn > 1e-14) ? (-sps * fast_rcp(zn)) : 1e300;
             const double t = fmin(t1, t2);
+            IST(3);  // step lengths
             if (!(t < 1e299)) {
                 status = WBC_QP_INFEASIBLE;
                 done = true;
@@ -1845,6 +1859,7 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
                     ++q;
                     select();  // the next row: slacks and active flags are final, J is not needed
                     householder_add(pos, d2, rk, zn, zk, dq, jq);
+                    IST(4);  // select + Householder add
                 } else {
                     // drop slot l1: shift the active lists, then Givens deletion (givens_drop) with the
                     // rotation of step k from the R column of the row now in slot k: (J^T n)[k, k+1]
@@ -1885,11 +1900,15 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
                         const double v = seg_shfl(rinv[k], src);
                         rinv[k] = (l < q && k >= l && k < q) ? v : 0.0;
                     }
+                    IST_COUNT(1);
                 }
                 mirror();
+                IST(5);  // mirror (and the drop path)
+                IST_COUNT(0);
             }
         }
     }
+    IST_FLUSH(a, rb);
     UST(a, rb, 16);  // active-set loop
     if (l < N) V.f[l] = x;
     lds_sync();

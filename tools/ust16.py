@@ -26,8 +26,9 @@ names = ["inputs+sincos", "stage A (leg chains)", "stage B (bodies)", "Jf + CoM 
 for i, n in enumerate(names):
     res[n] = float(np.median(u[ok, i + 1] - u[ok, i]))
 t10, t11 = st(10), st(11)
-gen = ok & (st(20) > 0) & (st(20) > t10)
-stn = ok & ~gen
+# the stance form stamps 19 (stance_reduce's leg inverses) inside its own reduce; the general form never
+stn = ok & (st(19) > t10) & (st(19) < t11)
+gen = ok & ~stn & (st(20) > t10)
 def med(a, b, m):
     return float(np.median(b[m] - a[m])) if m.any() else None
 res["general: R1-R4 (leg inverses, S6, S6^-1, Y, B, v, rho0)"] = med(t10, st(20), gen)
@@ -35,6 +36,9 @@ res["general: R5 (V, gamma, o, blk)"] = med(st(20), st(21), gen)
 res["general: R6 (H rows, g)"] = med(st(21), st(22), gen)
 res["general: R7 factor12 + R8 Nt"] = med(st(22), st(14), gen)
 res["stance: reduce + rank-6 factor"] = med(t10, t11, stn)
+for n, (i0, i1) in (("leg inverses, W", (None, 19)), ("S", (19, 20)), ("S^-1", (20, 12)), ("Y, q0", (12, 21)),
+                    ("Q = Y^T Y", (21, 22)), ("H^, g_f", (22, 13)), ("Nt, t0", (13, 14)), ("rank-6 factor", (14, 11))):
+    res[f"stance:   {n}"] = med(t10 if i0 is None else st(i0), st(i1), stn)
 for tag, m in (("general", gen), ("stance", stn)):
     if not m.any():
         continue
