@@ -189,11 +189,10 @@ void begin_update(wbc_engine* h, wbc::KernelArgs& a) {
 }
 
 // The default step (wbc_update_solve_kernel: every QP reduced to 12 variables and solved in the
-// update wave): it fills the fallback list of its parity like an elimination update
+// update wave) solves its own fallbacks in the wave that found them (no list), so it
+// leaves the fallback list and its parity to the split path's elimination updates.
 void begin_step16(wbc_engine* h, wbc::KernelArgs& a) {
     a.elim = 1;
-    a.parity = h->parity;
-    h->parity ^= 1;
     h->elim = false;  // a later wbc_solve needs its own wbc_update
 }
 

@@ -2086,65 +2086,98 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
     const double* qd = &s.in[13];
     const double* ref = &s.in[37];
 
-    // stage A: one lane per leg walks HAA -> HFE -> KFE; lane 4 writes the base frame.
-    // The joint-local factors (link rotation x joint rotation, axis in the parent frame) do not
-    // depend on the chain and are formed first, so each link adds one 3x3 product to the
-    // dependent chain instead of two.
-    if (lane < 4) {
-        const int l = lane;
-        double Lk[3][9], axl[3][3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const wbc_link& lk = md.link[l][k];
+    // stage A: the leg chains as prefix scans, one lane per joint: leg l, link k in lane 4 l + k
+    // (k < 3) of the robot's first DPP row; lane 4 l + 3 holds the base's values, so that row_ror:1
+    // hands link 0 the base as its parent.  The joint-local factors M_k = R_k^link axis_rot(q_k)
+    // do not depend on the chain; the link rotations are R_0 = R_B M_0, R_1 = R_B (M_0 M_1),
+    // R_2 = (R_B M_0)(M_1 M_2) (two rounds of 3x3 products instead of three in sequence), and the
+    // velocities / accelerations are sums over the links above (row_ror:1 / :2 under 0/1 masks):
+    //   w_k = w_B + sum_{m<=k} a_m qd_m, o_k = p_B + sum_{m<=k} rel_m, vo_k = v_B + sum_{m<=k} w_m^- x rel_m,
+    //   al_k = sum_{m<=k} (w_m^- x a_m) qd_m, ao_k = sum_{m<=k} al_m^- x rel_m + w_m^- x (w_m^- x rel_m)
+    // (rel_m = R_{m-1} p_m, a_m = R_{m-1} axis_m, ^- = before link m), the recursion of the
+    // reference's forward kinematics at nu_dot = 0.  Lane 3 writes the base frame.
+    static_assert(SUB == 16 || SUB == 64, "stage A uses the segment's first 16-lane DPP row");
+    {
+        const int l4 = (lane >> 2) & 3, k4 = lane & 3, kk = k4 < 3 ? k4 : 2, j = 3 * l4 + kk;
+        const bool base = (k4 == 3);
+        const wbc_link& lk = md.link[l4][kk];
+        const double m1 = (k4 >= 1 && !base) ? 1.0 : 0.0, m2 = (k4 >= 2 && !base) ? 1.0 : 0.0;
+        auto ror1 = [](double v) { return dpp_d<0x121>(v); };
+        auto ror2 = [](double v) { return dpp_d<0x122>(v); };
+        double RB[9], M[9], axl[3];
+        quat_R(s.in[3], s.in[4], s.in[5], s.in[6], RB);
+        {
             double Rl[9];
-            axis_rot(lk.axis, s.sc[3 * l + k][0], s.sc[3 * l + k][1], Rl);
-            mm3(lk.R, Rl, Lk[k]);
-            mv3(lk.R, lk.axis, axl[k]);
+            axis_rot(lk.axis, s.sc[j][0], s.sc[j][1], Rl);
+            mm3(lk.R, Rl, M);
+            mv3(lk.R, lk.axis, axl);
         }
-        double Rp[9], op[3], wp[3], alp[3] = {0, 0, 0}, aop[3] = {0, 0, 0}, vop[3];
-        quat_R(s.in[3], s.in[4], s.in[5], s.in[6], Rp);
 #pragma unroll
-        for (int i = 0; i < 3; ++i) { op[i] = pB[i]; wp[i] = wB[i]; vop[i] = vB[i]; }
+        for (int i = 0; i < 9; ++i) M[i] = base ? RB[i] : M[i];
+        // X = (parent's M, or R_B) M: R_0 in link 0, M_0 M_1 in link 1, M_1 M_2 in link 2
+        double P[9], X[9], R[9];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const wbc_link& lk = md.link[l][k];
-            const int j = 3 * l + k;
-            double rel[3], aj[3], t[3], u[3], Rn[9];
-            mv3(Rp, lk.p, rel);       // joint origin - parent origin (world)
-            mv3(Rp, axl[k], aj);      // joint axis (world)
-            mm3(Rp, Lk[k], Rn);       // child body orientation
-            const double qdk = qd[j];
-            // the joint origin is a point of the parent: velocity / acceleration at nu_dot = 0
-            cross3(wp, rel, t);
-            cross3(wp, t, u);
-            double ao[3];
-            cross3(alp, rel, ao);
+        for (int i = 0; i < 9; ++i) P[i] = ror1(M[i]);
+        mm3(P, M, X);
 #pragma unroll
-            for (int i = 0; i < 3; ++i) { vop[i] += t[i]; ao[i] += aop[i] + u[i]; }
-            cross3(wp, aj, t);
+        for (int i = 0; i < 9; ++i) X[i] = base ? RB[i] : X[i];
+        // R = (R_B, or X of link 0) X for links 1, 2
 #pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                alp[i] += t[i] * qdk;
-                wp[i] += aj[i] * qdk;
-                op[i] += rel[i];
-                aop[i] = ao[i];
-            }
+        for (int i = 0; i < 9; ++i) P[i] = ror2(X[i]);
+        mm3(P, X, R);
 #pragma unroll
-            for (int i = 0; i < 9; ++i) Rp[i] = Rn[i];
+        for (int i = 0; i < 9; ++i) R[i] = (k4 == 0 || base) ? X[i] : R[i];
+        // parent rotation: rel = R_{k-1} p_k, a = R_{k-1} axis_k
+        double rel[3], aj[3];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) P[i] = ror1(R[i]);
+        mv3(P, lk.p, rel);
+        mv3(P, axl, aj);
+        const double qdk = base ? 0.0 : qd[j];
+        auto excl = [&](const double* v, double* o) {  // sum over the links above (0 for link 0)
+#pragma unroll
+            for (int i = 0; i < 3; ++i) o[i] = fma(m2, ror2(v[i]), m1 * ror1(v[i]));
+        };
+        double c3[3], wex[3], t[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) c3[i] = aj[i] * qdk;
+        excl(c3, t);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) wex[i] = wB[i] + t[i];
+        double ope[3];
+        excl(rel, ope);
+        double tv[3], vex[3];
+        cross3(wex, rel, tv);
+        excl(tv, vex);
+        double at[3], alx[3];
+        cross3(wex, aj, at);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) at[i] *= qdk;
+        excl(at, alx);
+        double ot[3], u3[3], aox[3];
+        cross3(alx, rel, ot);
+        cross3(wex, tv, u3);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) ot[i] += u3[i];
+        excl(ot, aox);
+        if (lane < 16 && !base) {
             Frame& f = s.fr[1 + j];
 #pragma unroll
-            for (int i = 0; i < 9; ++i) f.R[i] = Rp[i];
+            for (int i = 0; i < 9; ++i) f.R[i] = R[i];
 #pragma unroll
             for (int i = 0; i < 3; ++i) {
-                f.o[i] = op[i]; f.w[i] = wp[i]; f.al[i] = alp[i]; f.ao[i] = aop[i]; f.vo[i] = vop[i];
-                s.ja[j][i] = aj[i]; s.jo[j][i] = op[i];
+                const double op = pB[i] + ope[i] + rel[i];
+                f.o[i] = op; f.w[i] = wex[i] + c3[i]; f.al[i] = alx[i] + at[i]; f.ao[i] = aox[i] + ot[i];
+                f.vo[i] = vB[i] + vex[i] + tv[i];
+                s.ja[j][i] = aj[i]; s.jo[j][i] = op;
             }
-        }
-    } else if (lane == 4) {
-        Frame& f = s.fr[0];
-        quat_R(s.in[3], s.in[4], s.in[5], s.in[6], f.R);
+        } else if (lane == 3) {
+            Frame& f = s.fr[0];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) { f.o[i] = pB[i]; f.w[i] = wB[i]; f.al[i] = 0.0; f.ao[i] = 0.0; f.vo[i] = vB[i]; }
+            for (int i = 0; i < 9; ++i) f.R[i] = RB[i];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) { f.o[i] = pB[i]; f.w[i] = wB[i]; f.al[i] = 0.0; f.ao[i] = 0.0; f.vo[i] = vB[i]; }
+        }
     }
     lds_sync();
 
@@ -4007,9 +4040,27 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_kernel(KernelArgs a) {
 // dynamics are recomputed per hypothesis segment: four hypotheses of one state share a wave's
 // instruction stream, and nothing passes through HBM).  update_phase reduces and solves the QP in
 // place (§4.6, §4.8); a QP whose reduction is not usable (a near-singular stance leg) writes its
-// problem to work row qp (no slot factor: presolved = 0) and goes to the fallback list, which
-// wbc_solve_fallback_kernel solves with the general 24-variable method (launched with modes = 0:
-// the record carries the QP's own mask and masked bounds).
+// problem to work row qp (no slot factor: presolved = 0), which the same wave then solves with the
+// general 24-variable method (drain_fallbacks, modes = 0: the record carries the QP's own mask and
+// masked bounds).
+__device__ void solve_general_qp(const KernelArgs& a, int rb, SolveLds& L);
+static_assert(sizeof(SolveLds) <= sizeof(UpdLds), "the drain reuses the update scratch");
+// A call (the rare path stays out of the kernel's register allocation), handed the address of the
+// kernel's arguments in its kernarg segment (passing the struct would pin a stack copy to the whole
+// kernel; a callee has no kernarg pointer of its own).
+__device__ __attribute__((noinline)) void drain_fallbacks(const KernelArgs* ka, unsigned long long fm, int qp0,
+                                                          SolveLds* L) {
+    KernelArgs f = *ka;
+    f.modes = 0;
+    f.elim = 0;
+    __threadfence_block();  // the records written above are read back by the whole wave
+    while (fm) {
+        const int seg = __builtin_ctzll(fm) / UPD_SUB;
+        fm &= fm - 1ull;
+        wsync();
+        solve_general_qp(f, qp0 + seg, *L);
+    }
+}
 WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) {
     __shared__ UpdLds L;
     const int seg = (int)threadIdx.x / UPD_SUB, lane = (int)threadIdx.x % UPD_SUB;
@@ -4022,9 +4073,12 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) {
     stage_to_lds<(int)(sizeof(wbc_model) / 8)>(reinterpret_cast<double*>(&L.model),
                                                 reinterpret_cast<const double*>(a.model), (int)threadIdx.x);
     lds_sync();
-    if (blockIdx.x == 0 && threadIdx.x == 0) a.fb[a.parity ^ 1] = 0;  // for the next step
     const bool solved = update_phase<UPD_SUB, true>(a, row, qp, kap, lane, wr, L.u[seg], L.prob[seg], nullptr, L.model);
-    if (wr && !solved) {
+    // a QP whose reduction was not usable: its problem goes to work row qp, and the wave solves it
+    // with the general 24-variable method right here (drain_fallbacks, the rare path; the wave's
+    // LDS is reused once the four segments are done)
+    const bool fb = wr && !solved;
+    if (fb) {
         const double2* src = reinterpret_cast<const double2*>(&L.prob[seg]);
         double* wrow = a.work + (size_t)qp * WORK_LEN;
         double2* dst = reinterpret_cast<double2*>(wrow);
@@ -4033,10 +4087,12 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) {
             Presolve* pre = reinterpret_cast<Presolve*>(wrow + PROB_LEN);
             pre->presolved = 0.0;
             pre->stance = 0.0;
-            const int idx = atomicAdd(&a.fb[a.parity], 1);
-            if (idx < a.fb_cap) a.fb[2 + idx] = qp;
         }
     }
+    const unsigned long long fm = __ballot(fb && lane == 0);
+    if (fm)
+        drain_fallbacks((const KernelArgs*)__builtin_amdgcn_kernarg_segment_ptr(), fm, (int)blockIdx.x * UPD_RPW,
+                        reinterpret_cast<SolveLds*>(&L));
 }
 
 // Four-contact QP whose equalities the update kernel eliminated (its Presolve::stance flag, in
@@ -4152,16 +4208,12 @@ extern "C" hipError_t wbc_launch_solve_stance(const wbc::KernelArgs* a, hipStrea
     hipLaunchKernelGGL(wbc::wbc_solve_fallback_kernel, dim3(16), dim3(64), 0, st, *a);
     return hipGetLastError();
 }
-// The default step in two launches: the update kernel reducing and solving every QP inline, then
-// the fallback kernel for the QPs whose reduction was not usable (their records carry their own
-// mask and bounds: the general solve runs them with modes = 0 and no stance-kernel skip).
+// The default step in one launch: the update kernel reducing and solving every QP inline, and the
+// QPs whose reduction was not usable with the general method in the same wave (drain_fallbacks:
+// their records carry their own mask and bounds, so the general solve runs them with modes = 0).
 extern "C" hipError_t wbc_launch_update_solve(const wbc::KernelArgs* a, hipStream_t st) {
     hipLaunchKernelGGL(wbc::wbc_update_solve_kernel, dim3((a->batch + wbc::UPD_RPW - 1) / wbc::UPD_RPW), dim3(64), 0,
                        st, *a);
-    wbc::KernelArgs f = *a;
-    f.modes = 0;
-    f.elim = 0;
-    hipLaunchKernelGGL(wbc::wbc_solve_fallback_kernel, dim3(16), dim3(64), 0, st, f);
     return hipGetLastError();
 }
 extern "C" hipError_t wbc_launch_reset(double* hist, const uint8_t* mask, int batch, hipStream_t st) {

@@ -99,6 +99,7 @@ struct KernelArgs {
     // instead of the general one).  QPs whose elimination did not happen (a near-singular leg)
     // are listed for the fallback solve: fb[parity] counts them, fb[2 ..] lists them (at most
     // fb_cap entries); the update kernel clears fb[parity ^ 1] for the next elimination update.
+    // (The default step, wbc_update_solve_kernel, solves its fallbacks in place and uses neither.)
     int32_t elim;
     int32_t parity;
     int32_t* fb;
