@@ -42,6 +42,20 @@ def stance_cold(B=4096, seed=1):
                 switching=np.ones(B, np.uint8))
 
 
+# Knee angle per leg at which the leg is stretched straight: its 3 x 3 foot Jacobian is singular
+# (|det| / max|J|^3 ~ 1e-13, whatever the hip angles; found by bisection on the lumped model).
+KNEE_STRAIGHT = np.array([-1.0, 1.0, 1.0, -1.0]) * 0.249494035113
+
+
+def straight_legs(inp, every=5):
+    """A copy of `inp` with one leg (leg b % 4) stretched straight on every `every`-th robot: the
+    stance elimination / 12-variable reduction is not usable there (the engine's fallback solve)."""
+    out = {k: np.array(v, copy=True) for k, v in inp.items()}
+    for b in range(0, len(out["qj"]), every):
+        out["qj"][b, 3 * (b % 4) + 2] = KNEE_STRAIGHT[b % 4]
+    return out
+
+
 def rl_random(B=65536, seed=3):
     """Config 4: randomized RL-style batch, contacts uniform over the 16 masks, cold."""
     g = np.random.default_rng(seed)

@@ -26,8 +26,8 @@ def test_fast_cpu_variant_matches_dense(name):
     if name == "stress":
         inp = _stress(192, 61)
     elif name == "straight_knees":
-        inp = workloads.stance_cold(64, seed=62)
-        inp["qj"][::3, 2] = 0.0  # a singular leg: the stance elimination falls back to the 24-variable form
+        # a singular (stretched) leg: the stance elimination falls back to the 24-variable form
+        inp = workloads.straight_legs(workloads.stance_cold(64, seed=62), every=3)
     else:
         inp = getattr(workloads, name)(256, seed=60)
     inp["switching"][:] = 1  # cold steps (the baseline's workloads)

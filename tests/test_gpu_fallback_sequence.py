@@ -23,10 +23,7 @@ def close(a, b, tol):
 
 
 def _steps(B):
-    st = workloads.stance_cold(B, seed=81)
-    straight = {k: v.copy() for k, v in st.items()}
-    for b in range(0, B, 5):  # a straight knee on one leg of every fifth robot: elimination fails
-        straight["qj"][b, 3 * (b % 4) + 2] = 0.0
+    straight = workloads.straight_legs(workloads.stance_cold(B, seed=81))  # fallbacks: stretched legs
     mixed1 = workloads.rl_random(B, seed=82)
     bent = workloads.stance_cold(B, seed=83)
     mixed2 = workloads.rl_random(B, seed=84)

@@ -138,8 +138,7 @@ def test_straight_knee_falls_back_and_matches_oracle():
     B = 96
     inp = workloads.stance_cold(B, seed=12)
     bent = inp["qj"].copy()
-    for b in range(0, B, 3):  # a straight knee on one leg of every third robot
-        inp["qj"][b, 3 * (b % 4) + 2] = 0.0
+    inp = workloads.straight_legs(inp, every=3)  # one leg stretched straight on every third robot
     out = run(inp)
     o = R.run_batch(inp)
     assert np.array_equal(out["status"], o["status"])

@@ -94,3 +94,24 @@ def test_c_reduced_form_stateful_trot_hotstart():
             it_hot += ob["iters"]
             it_cold += oc["iters"]
     assert it_hot < 0.5 * it_cold  # the hotstart keeps the rows that still exist across contact changes
+
+
+def test_straight_leg_makes_the_elimination_unusable():
+    """The fallback tests (test_gpu_fallback_sequence.py, test_gpu_stance_elim.py) stretch one leg of
+    every few robots straight: there the reduced form must be unusable (so the GPU's fallback solve
+    runs), and the C
+    oracle's REDUCED method, which falls back to the literal QP there, must agree with LITERAL."""
+    B = 40
+    inp = workloads.straight_legs(workloads.stance_cold(B, seed=81))
+    model = W.Model()
+    for b in range(B):
+        c = W.ReferenceWBC(model, {})
+        c.set_state(inp["base_pose"][b], inp["nu"][b], inp["qj"][b])
+        c.set_reference(inp["ref"][b], [(int(inp["contacts"][b]) >> i) & 1 for i in range(4)], bool(inp["switching"][b]))
+        c.update_state()
+        c.assemble_qp()
+        assert (RD.reduced_problem(c) is None) == (b % 5 == 0), b
+    a = R.run_batch(inp)
+    r = R.run_batch(inp, method=R.REDUCED)
+    fb = np.arange(B) % 5 == 0
+    assert np.array_equal(a["iters"][fb], r["iters"][fb]) and np.array_equal(a["status"], r["status"])
