@@ -1625,7 +1625,10 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
     int q = 0, pstar = -1, act = -1, ab = 0;  // ab: bit j = slot j of this lane active
     double u = 0.0, up = 0.0;
     bool done = (status != WBC_QP_OK);
-    const int max_wsr = pr.max_wsr;
+    int max_wsr = pr.max_wsr;
+    // held in a VGPR: left to the compiler it is re-loaded from the kernarg segment on every pass,
+    // and that scalar load's wait drains the pass's outstanding LDS reads
+    asm volatile("" : "+v"(max_wsr));
 
     // d = J^T n (lane j: dj = column j of the mirror . n), broadcast to every lane; d2 = rows >= pos;
     // r = R^-1 d (lane l < q), zn = |d2|^2, z = J2 d2 (lane k: z_k), dq = d[pos], jq = J[l][pos]
@@ -1808,11 +1811,15 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
                 for (int k = 0; k < N; ++k) a4[k & 3] = fma(jc[k], V.Nt[jt * 12 + k], a4[k & 3]);
                 const double dt = (a4[0] + a4[1]) + (a4[2] + a4[3]);
                 const double f0 = (rp == 0) ? -1.0 : (rp == 1 ? 1.0 : 0.0), f1 = (rp == 2) ? -1.0 : (rp == 3 ? 1.0 : 0.0);
-                double gl[4];
+                // one-hot weights instead of selects (a select chain here becomes branches that
+                // wait on the LDS reads): exactly one term below is nonzero
+                double df = ((l < N && !frc) ? ((tq & 1) ? 1.0 : -1.0) : 0.0) * dt;
 #pragma unroll
-                for (int L = 0; L < 4; ++L) gl[L] = fma(jc[3 * L], f0, fma(jc[3 * L + 1], f1, jc[3 * L + 2] * pr.friction));
-                const double df = sel4d(lg, gl[0], gl[1], gl[2], gl[3]);
-                dj = (l < N) ? (frc ? df : ((tq & 1) ? dt : -dt)) : 0.0;
+                for (int L = 0; L < 4; ++L) {
+                    const double gl = fma(jc[3 * L], f0, fma(jc[3 * L + 1], f1, jc[3 * L + 2] * pr.friction));
+                    df = fma((l < N && frc && lg == L) ? 1.0 : 0.0, gl, df);
+                }
+                dj = df;
             }
             const double sps = seg_shfl(sel3d(js, sp0, sp1, sp2), ol);
             IST(0);  // the chosen row's normal
@@ -2121,12 +2128,15 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
         mm3(P, M, X);
 #pragma unroll
         for (int i = 0; i < 9; ++i) X[i] = base ? RB[i] : X[i];
-        // R = (R_B, or X of link 0) X for links 1, 2
+        // R = (R_B, or X of link 0) X for links 1, 2; I X for link 0 and the base lanes (a select
+        // of the left factor, not of the product: the compiler turns the latter into branches)
+        const bool own = (k4 == 0 || base);
 #pragma unroll
-        for (int i = 0; i < 9; ++i) P[i] = ror2(X[i]);
+        for (int i = 0; i < 9; ++i) {
+            const double x2 = ror2(X[i]);
+            P[i] = own ? ((i % 4 == 0) ? 1.0 : 0.0) : x2;
+        }
         mm3(P, X, R);
-#pragma unroll
-        for (int i = 0; i < 9; ++i) R[i] = (k4 == 0 || base) ? X[i] : R[i];
         // parent rotation: rel = R_{k-1} p_k, a = R_{k-1} axis_k
         double rel[3], aj[3];
 #pragma unroll
