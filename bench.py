@@ -3,8 +3,8 @@
 
 One step = one wbc_step over the rank's batch (dynamics + centroidal assembly + QP + torques: one
 kernel, wbc_update_solve_kernel, four QPs per wave, each reduced exactly to 12 variables and
-solved in place; plus the near-empty fallback launch), plus for N > 1 the RCCL all-gather of the
-torque block.  Inputs are
+solved in place; a QP whose reduction is not usable is solved by the same wave's general method),
+plus for N > 1 the RCCL all-gather of the torque block.  Inputs are
 resident in HBM before the timed region.  Default workload: configs[1] of BASELINE.json,
 B = 4096 four-contact stance states, cold solves, per GPU (weak scaling).
 
@@ -235,7 +235,7 @@ def bench_trot(torch, stream, device, STATELESS, B=4096, T=400, seed=2):
     e.close()
     its = np.stack(its)
     rl = roofline_of(step_flops(B * T, its) / T, ms / T)
-    rl["note"] = "per step (one wbc_update_solve_kernel launch + the fallback launch): flops of the 400-step " \
+    rl["note"] = "per step (one wbc_update_solve_kernel launch): flops of the 400-step " \
                  "sequence / 400 over the sequence's HIP-event time / 400"
     return dict(batch=B, steps=T, ms_total=ms, ms_per_step=ms / T, solves_per_s=B * T / (ms * 1e-3),
                 wall_solves_per_s=B * T / wall, status_counts_last=np.bincount(o["status"], minlength=4).tolist(),
@@ -425,9 +425,8 @@ def main():
         return ev0.elapsed_time(ev1) / args.steps
 
     # A step is one kernel (wbc_update_solve_kernel: dynamics, the QP reduced to 12 variables and
-    # solved in the same wave, torques) plus the elimination-fallback kernel, near empty (no
-    # near-singular legs in the bench states): the step's time is that kernel's, with the empty launch
-    # behind it (rocprofv3 in profiles/ separates the two).  It owns all of SURVEY 8(d)'s flops.
+    # solved in the same wave, torques; the rare unusable reduction solved there too by the general
+    # method): the step's time is that kernel's.  It owns all of SURVEY 8(d)'s flops.
     step_ms = timed(lambda: step(STEP_FLAGS))
     out = e.outputs()
     iters = out["iters"].astype(np.int64)
@@ -467,10 +466,6 @@ def main():
             e2.close()
 
     traffic, traffic_src = committed_traffic(args.config, B)
-    if traffic:  # the fallback kernel (near empty) is part of the step
-        traffic = dict(traffic)
-        traffic["wbc_update_solve_kernel"] = (traffic.get("wbc_update_solve_kernel") or 0.0) + \
-            (traffic.get("wbc_solve_fallback_kernel") or 0.0)
     total = (B * world if scaling == "weak" else B_total) * args.steps
     value = total / elapsed
     result = {
@@ -495,8 +490,8 @@ def main():
                      "frac": tf_dom / FP64_PEAK_TFLOPS, "traffic": traffic.get(dom),
                      "traffic_source": traffic_src, "kernel": dom, "kernel_ms": dom_ms,
                      "kernels_ms": kernels, "step_kernels_ms": step_ms,
-                     "note": "the step's one kernel (wbc_update_solve_kernel; its kernel_ms is the step's, with "
-                             "the near-empty fallback launch); fp64 VALU roof (no MFMA on this path; gfx950 fp64 "
+                     "note": "the step's one kernel (wbc_update_solve_kernel; its kernel_ms is the step's, HIP events "
+                             "around back-to-back launches); fp64 VALU roof (no MFMA on this path; gfx950 fp64 "
                              "vector peak); SURVEY 8(d) algorithmic flops: F_dyn + F_asm per state, F_fact + F_tau + "
                              "k F_iter per QP, k = iters[] (working-set changes of the 12-variable form the engine "
                              "solves); latency/issue-bound small dense linear algebra",
