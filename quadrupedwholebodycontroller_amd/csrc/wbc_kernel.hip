@@ -4071,10 +4071,18 @@ __device__ __attribute__((noinline)) void drain_fallbacks(const KernelArgs* ka, 
         solve_general_qp(f, qp0 + seg, *L);
     }
 }
+// Workgroups are dispatched to the 8 XCDs round-robin (block b on XCD b % 8), each with its own
+// L2.  Under mode hypotheses the K / 4 workgroups of one state read the same input rows, so each
+// XCD gets a contiguous range of logical blocks: a state's workgroups share one L2 and its inputs
+// come from HBM once.
+__device__ __forceinline__ int xcd_block(int b, int n) {
+    const int x = b & 7, i = b >> 3, per = n >> 3, rem = n & 7;  // XCD x runs per + (x < rem) blocks
+    return x * per + min(x, rem) + i;
+}
 WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) {
     __shared__ UpdLds L;
     const int seg = (int)threadIdx.x / UPD_SUB, lane = (int)threadIdx.x % UPD_SUB;
-    int qp = (int)blockIdx.x * UPD_RPW + seg;
+    int qp = (a.modes ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x) * UPD_RPW + seg;
     const bool wr = qp < a.batch;  // a padding segment recomputes the last QP, writes nothing
     if (!wr) qp = a.batch - 1;
     const int K = a.modes;
