@@ -99,22 +99,19 @@ struct St16 {
     double* Bt;    // [12][6]  phi = B z: column j of B (ja, jo)
     double* Vt;    // [12][6]  leg row i: its coupling v_i to phi (in)
     double* rho0;  // [12]     leg row i at z = 0 (in + 72)
-    double* Ct;    // [12][6]  P_j (stance slot) or o_j (swing slot), Hessian assembly (Mjj, hj, cen)
     double* J0;    // [12][12] copy of the initial J rows for a rejected hotstart (P.Mbj)
-    __device__ explicit St16(UpdScratch& s)
+    const double* fric;  // [16][12] the friction faces' normals (the workgroup's shared table)
+    __device__ St16(UpdScratch& s, const double* fr)
         : Nt(&s.ja[0][0]), Y(&s.in[0]), t0(&s.in[72]), q0(&s.sc[0][0]), nsel(&s.sc[6][0]), col(&s.KA[0][0]),
-          f(&s.cen[0]), Bt(nullptr), Vt(nullptr), rho0(nullptr), Ct(nullptr), J0(nullptr) {}
-    __device__ St16(UpdScratch& s, Prob& P)
+          f(&s.cen[0]), Bt(nullptr), Vt(nullptr), rho0(nullptr), J0(nullptr), fric(fr) {}
+    __device__ St16(UpdScratch& s, Prob& P, const double* fr)
         : Nt(&P.Jbj[0]), Y(&s.sr.Y[0][0]), t0(&s.pf[0][0]), q0(&s.sr.q0[0]), nsel(&s.sc[6][0]), col(&s.KA[0][0]),
-          f(&s.KA[0][0] + 16), Bt(&s.ja[0][0]), Vt(&s.in[0]), rho0(&s.in[72]), Ct(&s.Mjj[0][0]), J0(&P.Mbj[0]) {}
+          f(&s.KA[0][0] + 16), Bt(&s.ja[0][0]), Vt(&s.in[0]), rho0(&s.in[72]), J0(&P.Mbj[0]), fric(fr) {}
 };
 static_assert(offsetof(UpdScratch, A) + sizeof(UpdScratch::A) - offsetof(UpdScratch, ja) >= 144 * sizeof(double), "St16 Nt");
 static_assert(offsetof(UpdScratch, jo) == offsetof(UpdScratch, ja) + sizeof(UpdScratch::ja), "St16 Bt");
 static_assert(offsetof(UpdScratch, vf) == offsetof(UpdScratch, pf) + sizeof(UpdScratch::pf), "St16 t0");
 static_assert(sizeof(UpdScratch::KA) >= 28 * sizeof(double), "St16 col / f");
-static_assert(offsetof(UpdScratch, hj) == offsetof(UpdScratch, Mjj) + sizeof(UpdScratch::Mjj) &&
-              offsetof(UpdScratch, cen) == offsetof(UpdScratch, hj) + sizeof(UpdScratch::hj) &&
-              sizeof(UpdScratch::Mjj) + sizeof(UpdScratch::hj) + sizeof(UpdScratch::cen) >= 72 * sizeof(double), "St16 Ct");
 
 struct QpScratch {
     static constexpr int N = NQ;
@@ -941,7 +938,7 @@ __device__ bool stance_reduce([[maybe_unused]] const KernelArgs& ka, [[maybe_unu
             for (int kj = 0; kj < 3; ++kj) nt[3 * lj + kj] = mm[kj] - cr[kj] + P.Jbj[(3 * lj + kj) * 12 + j];
         }
         if constexpr (SOLVE) {
-            const St16 V(s);
+            const St16 V(s, nullptr);
             if (lane < 12) {
 #pragma unroll
                 for (int c = 0; c < 12; c += 2)
@@ -1799,27 +1796,19 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
         if (!done) {
             const int pos = q, ol = pstar & 15, js = pstar >> 4;
             // dj = column j of J . n for the chosen row, from the row id alone (no exchange of its
-            // normal through the owner lane): a torque row is +-row jt of Nt (LDS, one address per
-            // segment), a friction face -D[rp] = (f0, f1, mu) on leg lg's slot; the slack from the
-            // owner lane
+            // normal through the owner lane): a torque row is +-row of Nt, a friction face a row of
+            // the workgroup's normal table (LDS, one address per segment); the slack from the owner
+            // lane
             double dj;
             {
                 const bool frc = pstar < 16;
-                const int tq = pstar - 16, jt = frc ? 0 : (tq >> 1), rp = pstar & 3, lg = (pstar >> 2) & 3;
+                const int tq = pstar - 16;
+                const double* nrow = frc ? &V.fric[pstar * 12] : &V.Nt[(tq >> 1) * 12];
                 double a4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-                for (int k = 0; k < N; ++k) a4[k & 3] = fma(jc[k], V.Nt[jt * 12 + k], a4[k & 3]);
-                const double dt = (a4[0] + a4[1]) + (a4[2] + a4[3]);
-                const double f0 = (rp == 0) ? -1.0 : (rp == 1 ? 1.0 : 0.0), f1 = (rp == 2) ? -1.0 : (rp == 3 ? 1.0 : 0.0);
-                // one-hot weights instead of selects (a select chain here becomes branches that
-                // wait on the LDS reads): exactly one term below is nonzero
-                double df = ((l < N && !frc) ? ((tq & 1) ? 1.0 : -1.0) : 0.0) * dt;
-#pragma unroll
-                for (int L = 0; L < 4; ++L) {
-                    const double gl = fma(jc[3 * L], f0, fma(jc[3 * L + 1], f1, jc[3 * L + 2] * pr.friction));
-                    df = fma((l < N && frc && lg == L) ? 1.0 : 0.0, gl, df);
-                }
-                dj = df;
+                for (int k = 0; k < N; ++k) a4[k & 3] = fma(jc[k], nrow[k], a4[k & 3]);
+                const double dn = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+                dj = ((l < N) ? ((frc || (tq & 1)) ? 1.0 : -1.0) : 0.0) * dn;
             }
             const double sps = seg_shfl(sel3d(js, sp0, sp1, sp2), ol);
             IST(0);  // the chosen row's normal
@@ -2021,7 +2010,7 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
 // the general fallback solve).  !SOLVE: the split update (Prob + Presolve records to HBM).
 template <int SUB, bool SOLVE = false>
 __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int lane, bool wr, UpdScratch& s, Prob& P,
-                             Presolve* pre, const wbc_model& md) {
+                             Presolve* pre, const wbc_model& md, const double* fric = nullptr) {
     const wbc_params& pr = a.pv;
     const bool switching = a.switching[rb] != 0;
     const bool stateful = a.stateful != 0;
@@ -2697,12 +2686,12 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
             double hrow[12], gsv = 0.0;
             if (stance_reduce<true>(a, rb, P, pr, lane, wr, s, hrow, gsv, nullptr) && rank6_factor(P, s, gsv, lane)) {
                 UST(a, rb, 11);
-                solve16<true, false>(a, rb, qp, lane, wr, P, s, St16(s), 15, WBC_QP_OK);
+                solve16<true, false>(a, rb, qp, lane, wr, P, s, St16(s, fric), 15, WBC_QP_OK);
                 return true;
             }
             return false;
         }
-        const St16 V(s, P);
+        const St16 V(s, P, fric);
         bool vac = false;
         if (reduce_general(a, rb, P, pr, lane, kap, s, V, vac)) {
             UST(a, rb, 11);
@@ -3948,9 +3937,12 @@ __device__ void solve_stance(const KernelArgs& a, int rb, const Prob* Pg, const 
 constexpr int UPD_SUB = 16, UPD_RPW = 64 / UPD_SUB;
 struct UpdLds {
     wbc_model model;  // staged once per wave: the kinematic chain reads it at lane-varying addresses
+    double fric[16][12];  // normals of the 16 friction faces (face 4 l + rr: -D[rr] on leg l's slot)
     Prob prob[UPD_RPW];
     UpdScratch u[UPD_RPW];
 };
+// four workgroups per CU (one wave per SIMD): 160 KB of LDS
+static_assert(4 * sizeof(UpdLds) <= 160 * 1024, "update_solve LDS budget");
 struct SolveLds {
     Prob prob;
     QpScratch q;
@@ -4090,8 +4082,16 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) {
     const int kap = (K ? a.mode_masks[qp - row * K] : a.contacts[row]) & 15;
     stage_to_lds<(int)(sizeof(wbc_model) / 8)>(reinterpret_cast<double*>(&L.model),
                                                 reinterpret_cast<const double*>(a.model), (int)threadIdx.x);
+#pragma unroll
+    for (int e = (int)threadIdx.x; e < 192; e += 64) {
+        const int p = e / 12, k = e % 12, rr = p & 3, r = k % 3;
+        const double fv = (r == 0) ? ((rr == 0) ? -1.0 : (rr == 1 ? 1.0 : 0.0))
+                        : (r == 1) ? ((rr == 2) ? -1.0 : (rr == 3 ? 1.0 : 0.0)) : a.pv.friction;
+        L.fric[p][k] = (k / 3 == (p >> 2)) ? fv : 0.0;
+    }
     lds_sync();
-    const bool solved = update_phase<UPD_SUB, true>(a, row, qp, kap, lane, wr, L.u[seg], L.prob[seg], nullptr, L.model);
+    const bool solved = update_phase<UPD_SUB, true>(a, row, qp, kap, lane, wr, L.u[seg], L.prob[seg], nullptr, L.model,
+                                                    &L.fric[0][0]);
     // a QP whose reduction was not usable: its problem goes to work row qp, and the wave solves it
     // with the general 24-variable method right here (drain_fallbacks, the rare path; the wave's
     // LDS is reused once the four segments are done)
