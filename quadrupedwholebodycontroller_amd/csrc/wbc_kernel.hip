@@ -1528,11 +1528,18 @@ __device__ __forceinline__ double tag6(double v, int idx) {
     const int tag = (hi < 0) ? (63 - idx) : idx;
     return __hiloint2double(hi, (__double2loint(v) & ~63) | tag);
 }
+// v_min_f64 without fmin's quieting of its DPP-moved operand (a v_max_f64 x, x per step): the
+// values reduced here are never NaN (1e300 marks "none"), and v_min_f64 is IEEE minNum anyway
+__device__ __forceinline__ double vmin_f64(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 __device__ __forceinline__ double seg16_min(double v) {
-    v = fmin(v, dpp_d<0x128>(v));
-    v = fmin(v, dpp_d<0x124>(v));
-    v = fmin(v, dpp_d<0x122>(v));
-    v = fmin(v, dpp_d<0x121>(v));
+    v = vmin_f64(v, dpp_d<0x128>(v));
+    v = vmin_f64(v, dpp_d<0x124>(v));
+    v = vmin_f64(v, dpp_d<0x122>(v));
+    v = vmin_f64(v, dpp_d<0x121>(v));
     return v;
 }
 __device__ __forceinline__ int untag6(double v) {
@@ -1635,10 +1642,18 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
         for (int k = 0; k < N; ++k) acc[k & 3] += jc[k] * np[k];
         return (l < N) ? (acc[0] + acc[1]) + (acc[2] + acc[3]) : 0.0;
     };
+    // d is broadcast in its two parts, masked at the source lane (one select there instead of a mask
+    // per element in every lane): d1 = rows < pos (the active part; rows of R^-1 are 0 beyond q =
+    // pos anyway) and d2 = rows >= pos
     auto direction = [&](double dj, int pos, double* d2, double& rk, double& zn, double& zk, double& dq, double& jq) {
-        double d[N];
+        const double dj2 = (l >= pos) ? dj : 0.0;
+        const double dj1 = dj - dj2;
+        double d1[N];
 #pragma unroll
-        for (int k = 0; k < N; ++k) d[k] = seg_bcast<16>(dj, k);
+        for (int k = 0; k < N; ++k) {
+            d1[k] = seg_bcast<16>(dj1, k);
+            d2[k] = seg_bcast<16>(dj2, k);
+        }
         // d[pos] and J[l][pos] (needed only by the Householder add, so their LDS latency is off
         // the chain): from lane pos of the segment and from the J mirror
         dq = seg_shfl(dj, pos);  // lane 12.. holds 0
@@ -1647,10 +1662,8 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
             double acc[4] = {0.0, 0.0, 0.0, 0.0}, zz[4] = {0, 0, 0, 0};
 #pragma unroll
             for (int j = 0; j < N; ++j) {
-                const double mk = (j >= pos) ? 1.0 : 0.0;
-                acc[j & 3] += rinv[j] * d[j];
-                d2[j] = d[j] * mk;
-                zz[j & 3] += d[j] * d2[j];
+                acc[j & 3] += rinv[j] * d1[j];
+                zz[j & 3] += d2[j] * d2[j];
             }
             rk = (l < N) ? (acc[0] + acc[1]) + (acc[2] + acc[3]) : 0.0;
             zn = (zz[0] + zz[1]) + (zz[2] + zz[3]);
