@@ -156,7 +156,10 @@ int32_t wbc_create(const wbc_model* model, const wbc_params* params, int32_t bat
 int32_t wbc_destroy(wbc_engine* h);
 int32_t wbc_batch(const wbc_engine* h);
 /* Use a caller-owned hipStream_t (NULL = the engine's own stream).  Work queued on the previous
- * stream is drained first (the call synchronizes it), so switching streams never races. */
+ * stream is drained first (the call synchronizes it), so switching streams never races.  A bound
+ * caller stream must stay alive until it is unbound (wbc_set_stream(h, NULL)) or the engine is
+ * destroyed: both synchronize it.  (No event is recorded after each launch to track the stream:
+ * its packet would cost ~3 us per step.) */
 int32_t wbc_set_stream(wbc_engine* h, void* hip_stream);
 
 /* Host inputs, copied to device on the engine stream. Any pointer may be NULL (= unchanged). */

@@ -95,8 +95,6 @@ struct wbc_engine {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // last launch on a caller's stream (wbc_set_stream): the engine waits for this event, not for
     // the stream (which the caller may destroy) or the device (other engines' and torch's work)
-    hipEvent_t done_ev = nullptr;
-    bool done_pending = false;
     double last_ms = 0.0;
 };
 
@@ -149,21 +147,11 @@ wbc::KernelArgs make_args(wbc_engine* h, uint32_t flags) {
     return a;
 }
 
-// after the launches of an API call: on a caller's stream, remember where they end
-hipError_t note_launch(wbc_engine* h) {
-    if (h->stream == h->own_stream) return hipSuccess;
-    h->done_pending = true;
-    return hipEventRecord(h->done_ev, h->stream);
-}
-
-// wait for every launch the engine queued so far (its own stream, or the caller's up to done_ev)
-hipError_t drain(wbc_engine* h) {
-    if (h->stream == h->own_stream) return h->own_stream ? hipStreamSynchronize(h->own_stream) : hipSuccess;
-    if (!h->done_pending) return hipSuccess;
-    const hipError_t e = hipEventSynchronize(h->done_ev);
-    if (e == hipSuccess) h->done_pending = false;
-    return e;
-}
+// wait for every launch the engine queued so far: a stream synchronize of the bound stream (its
+// own, or the caller's, which must still be alive: include/wbc.h, wbc_set_stream).  No event is
+// recorded per launch: an event packet between two steps costs ~3 us of the ~36 us step (measured
+// on MI355X, 103.5 -> 112.3 M solves/s on the headline config without it).
+hipError_t drain(wbc_engine* h) { return h->stream ? hipStreamSynchronize(h->stream) : hipSuccess; }
 
 int64_t count_stance(const uint8_t* masks, size_t n) {
     int64_t c = 0;
@@ -286,8 +274,7 @@ int32_t wbc_create(const wbc_model* model, const wbc_params* params, int32_t bat
     ALLOC(d_dbg, B * WBC_DBG_LEN);
 #undef ALLOC
     if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess ||
-        hipEventCreateWithFlags(&h->done_ev, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) {
         wbc_destroy(h);
         return fail(WBC_ERR_HIP, "stream/event creation failed");
     }
@@ -331,9 +318,8 @@ int32_t wbc_create(const wbc_model* model, const wbc_params* params, int32_t bat
 int32_t wbc_destroy(wbc_engine* h) {
     if (!h) return WBC_OK;
     (void)hipSetDevice(h->device);
-    // drain the engine's in-flight work before freeing: its own stream, or the event recorded
-    // after its last launch on a caller's stream (which may be destroyed by now); never the whole
-    // device, which would also wait for other engines' and the caller's unrelated work
+    // drain the engine's in-flight work before freeing (the bound stream; never the whole device,
+    // which would also wait for other engines' and the caller's unrelated work)
     (void)drain(h);
     void* ptrs[] = {h->d_model, h->d_params, h->d_inblk, h->d_outblk, h->d_mask, h->d_modes, h->d_hist, h->d_work,
                     h->d_fb, h->d_dbg};
@@ -343,7 +329,6 @@ int32_t wbc_destroy(wbc_engine* h) {
     if (h->h_out) (void)hipHostFree(h->h_out);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
-    if (h->done_ev) (void)hipEventDestroy(h->done_ev);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
     return WBC_OK;
@@ -356,13 +341,11 @@ int32_t wbc_set_stream(wbc_engine* h, void* stream) {
     const hipStream_t next = stream ? reinterpret_cast<hipStream_t>(stream) : h->own_stream;
     if (next != h->stream) {
         // work already queued on the old stream still reads the engine's buffers: let it finish
-        // before any call on the new stream can overwrite them (through the event after its last
-        // launch when the old stream is a caller's, so a caller stream destroyed since is safe)
+        // before any call on the new stream can overwrite them
         WBC_HIP(hipSetDevice(h->device));
         WBC_HIP(drain(h));
     }
     h->stream = next;
-    h->done_pending = false;
     return WBC_OK;
 }
 
@@ -425,7 +408,6 @@ int32_t wbc_reset(wbc_engine* h, const uint8_t* mask) {
     }
     WBC_HIP(wbc_launch_reset(h->d_hist, dm, h->batch, h->stream));
     WBC_HIP(hipStreamSynchronize(h->stream));
-    h->done_pending = false;
     h->updated = false;
     return WBC_OK;
 }
@@ -437,7 +419,6 @@ int32_t wbc_update(wbc_engine* h, uint32_t flags) {
     wbc::KernelArgs a = make_args(h, flags);
     begin_update(h, a);
     WBC_HIP(wbc_launch_update(&a, h->stream));
-    WBC_HIP(note_launch(h));
     h->updated = true;
     return WBC_OK;
 }
@@ -449,7 +430,6 @@ int32_t wbc_solve(wbc_engine* h, uint32_t flags) {
     WBC_HIP(hipSetDevice(h->device));
     wbc::KernelArgs a = make_args(h, flags);
     WBC_HIP(launch_solves(h, a));
-    WBC_HIP(note_launch(h));
     return WBC_OK;  // the assembled problem stays valid: solving it again gives the same result
 }
 
@@ -476,7 +456,6 @@ int32_t wbc_step(wbc_engine* h, uint32_t flags) {
         WBC_HIP(hipEventRecord(h->ev1, h->stream));
         h->timed = true;
     }
-    WBC_HIP(note_launch(h));
     h->updated = false;
     return WBC_OK;
 }
@@ -526,7 +505,6 @@ int32_t wbc_step_modes(wbc_engine* h, uint32_t flags) {
         WBC_HIP(hipEventRecord(h->ev1, h->stream));
         h->timed = true;
     }
-    WBC_HIP(note_launch(h));
     h->updated = false;
     return WBC_OK;
 }

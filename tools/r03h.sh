@@ -2,7 +2,7 @@
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/r03h
 O=gpurun_out/r03h
-timeout -k 10 300 python -u -m pytest tests/test_gpu_iters.py tests/test_gpu_parity.py tests/test_gpu_stateful.py tests/test_gpu_modes.py tests/test_gpu_fallback_sequence.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_iters.py tests/test_gpu_parity.py tests/test_gpu_stateful.py tests/test_gpu_modes.py tests/test_gpu_fallback_sequence.py tests/test_gpu_stream.py tests/test_gpu_controller.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 timeout -k 10 300 python bench.py --steps 50 --warmup 5 --extra --no-cpu-baseline > $O/bench.log 2>&1 || { tail $O/bench.log; exit 1; }
 python3 - <<'PY'
