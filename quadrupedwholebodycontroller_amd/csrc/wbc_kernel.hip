@@ -2021,9 +2021,25 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
 // here too (solve16: the four-contact stance form on stateless all-stance waves, the general form
 // otherwise); returns false when the reduction was not usable (the caller writes the problem for
 // the general fallback solve).  !SOLVE: the split update (Prob + Presolve records to HBM).
+// the robot's 91 input doubles (pose | nu | q | ref), SUB lanes, element lane + it * SUB in v[it]
+template <int SUB>
+__device__ __forceinline__ void load_inputs(const KernelArgs& a, int rb, int lane, double (&v)[(91 + SUB - 1) / SUB]) {
+    constexpr int NIT = (91 + SUB - 1) / SUB;
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+        const int k = (lane + it * SUB < 91) ? lane + it * SUB : 90;
+        const double* p = (k < 7) ? a.base_pose + (size_t)rb * 7 + k
+                        : (k < 25) ? a.nu + (size_t)rb * 18 + (k - 7)
+                        : (k < 37) ? a.qj + (size_t)rb * 12 + (k - 25)
+                                   : a.ref + (size_t)rb * 54 + (k - 37);
+        v[it] = *p;
+    }
+}
+
 template <int SUB, bool SOLVE = false>
 __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int lane, bool wr, UpdScratch& s, Prob& P,
-                             Presolve* pre, const wbc_model& md, const double* fric = nullptr) {
+                             Presolve* pre, const wbc_model& md, const double* fric = nullptr,
+                             const double* vin = nullptr) {
     const wbc_params& pr = a.pv;
     const bool switching = a.switching[rb] != 0;
     const bool stateful = a.stateful != 0;
@@ -2056,17 +2072,15 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
         if (lane == 0) { P.flags = anybad ? 1.0 : 0.0; P.kappa = (double)kap; }
     } else {
         // all loads issued before any is used (addresses clamped to element 90, so every lane
-        // loads); the joint angles' sin / cos come from LDS after the exchange
+        // loads); the joint angles' sin / cos come from LDS after the exchange.  vin: the caller
+        // issued them already (load_inputs, before its own staging loads: one HBM round trip)
         constexpr int NIT = (91 + SUB - 1) / SUB;
         double v[NIT];
+        if (vin) {
 #pragma unroll
-        for (int it = 0; it < NIT; ++it) {
-            const int k = (lane + it * SUB < 91) ? lane + it * SUB : 90;
-            const double* p = (k < 7) ? a.base_pose + (size_t)rb * 7 + k
-                            : (k < 25) ? a.nu + (size_t)rb * 18 + (k - 7)
-                            : (k < 37) ? a.qj + (size_t)rb * 12 + (k - 25)
-                                       : a.ref + (size_t)rb * 54 + (k - 37);
-            v[it] = *p;
+            for (int it = 0; it < NIT; ++it) v[it] = vin[it];
+        } else {
+            load_inputs<SUB>(a, rb, lane, v);
         }
         bool bad = false;
 #pragma unroll
@@ -4093,6 +4107,9 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) {
     const int K = a.modes;
     const int row = K ? qp / K : qp;
     const int kap = (K ? a.mode_masks[qp - row * K] : a.contacts[row]) & 15;
+    // the robot's inputs (HBM) are requested before the model staging waits for its own loads
+    double vin[(91 + UPD_SUB - 1) / UPD_SUB];
+    load_inputs<UPD_SUB>(a, row, lane, vin);
     stage_to_lds<(int)(sizeof(wbc_model) / 8)>(reinterpret_cast<double*>(&L.model),
                                                 reinterpret_cast<const double*>(a.model), (int)threadIdx.x);
 #pragma unroll
@@ -4104,7 +4121,7 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) {
     }
     lds_sync();
     const bool solved = update_phase<UPD_SUB, true>(a, row, qp, kap, lane, wr, L.u[seg], L.prob[seg], nullptr, L.model,
-                                                    &L.fric[0][0]);
+                                                    &L.fric[0][0], vin);
     // a QP whose reduction was not usable: its problem goes to work row qp, and the wave solves it
     // with the general 24-variable method right here (drain_fallbacks, the rare path; the wave's
     // LDS is reused once the four segments are done)
