@@ -1684,14 +1684,20 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
         const double ia = (dq >= 0.0) ? -rs : rs;
         const double beta = fast_rcp(zn + nrm2 * fabs(dq));
         const double vw = (zk - alpha * jq) * beta, vwa = vw * alpha;
+        // the unit vector e_pos, broadcast from the lanes (lane pos holds 1): one DPP move per
+        // element instead of a compare + select + move per element in every lane
+        const double epl = (l == pos) ? 1.0 : 0.0;
+        double ep[N];
 #pragma unroll
-        for (int k = 0; k < N; ++k) Jr[k] = fma(vwa, (k == pos) ? 1.0 : 0.0, fma(-vw, d2[k], Jr[k]));
+        for (int k = 0; k < N; ++k) ep[k] = seg_bcast<16>(epl, k);
+#pragma unroll
+        for (int k = 0; k < N; ++k) Jr[k] = fma(vwa, ep[k], fma(-vw, d2[k], Jr[k]));
         const double nv = (l == pos) ? ia : -rk * ia;
         // column pos of R^-1 is 0 before the add and nv is finite here (zn > 1e-14), so adding nv
         // under the 0 / 1 mask is exact
         const double nvw = (l <= pos) ? nv : 0.0;
 #pragma unroll
-        for (int k = 0; k < N; ++k) rinv[k] = fma((k == pos) ? 1.0 : 0.0, nvw, rinv[k]);
+        for (int k = 0; k < N; ++k) rinv[k] = fma(ep[k], nvw, rinv[k]);
     };
 
     // Hotstart (qpOASES SQProblem::hotstart, cpp:529-533): the previous solve's working set (row
@@ -4104,6 +4110,7 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) {
     int qp = (a.modes ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x) * UPD_RPW + seg;
     const bool wr = qp < a.batch;  // a padding segment recomputes the last QP, writes nothing
     if (!wr) qp = a.batch - 1;
+    UST(a, qp, 30);  // kernel entry (diagnostic build)
     const int K = a.modes;
     const int row = K ? qp / K : qp;
     const int kap = (K ? a.mode_masks[qp - row * K] : a.contacts[row]) & 15;

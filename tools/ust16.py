@@ -35,6 +35,7 @@ res["general: R1-R4 (leg inverses, S6, S6^-1, Y, B, v, rho0)"] = med(t10, st(20)
 res["general: R5 (V, gamma, o, blk)"] = med(st(20), st(21), gen)
 res["general: R6 (H rows, g)"] = med(st(21), st(22), gen)
 res["general: R7 factor12 + R8 Nt"] = med(st(22), st(14), gen)
+res["prologue (kernel entry -> update start: model staging, input loads)"] = float(np.median((st(0) - st(30))[ok]))
 res["stance: reduce + rank-6 factor"] = med(t10, t11, stn)
 for n, (i0, i1) in (("leg inverses, W", (None, 19)), ("S", (19, 20)), ("S^-1", (20, 12)), ("Y, q0", (12, 21)),
                     ("Q = Y^T Y", (21, 22)), ("H^, g_f", (22, 13)), ("Nt, t0", (13, 14)), ("rank-6 factor", (14, 11))):
@@ -46,6 +47,8 @@ for tag, m in (("general", gen), ("stance", stn)):
     res[f"{tag}: active-set loop"] = med(st(15), st(16), m)
     res[f"{tag}: primal + outputs"] = med(st(16), st(18), m)
     res[f"{tag}: total"] = med(st(0), st(18), m)
+    res[f"{tag}: entry to end"] = med(st(30), st(18), m)
+    res[f"{tag}: entry to end, max over waves"] = float(np.max((st(18) - st(30))[m]))
 out = e.outputs()
 wi = out["iters"][: (B // 4) * 4].reshape(-1, 4).max(1)
 res["mean max-over-wave iters"] = float(wi.mean())
