@@ -118,7 +118,7 @@ public:
     // updateState(); solveQP(); computeJointTorques(); as one engine call (wbc_cycle: one H2D copy,
     // the step's kernels, one D2H copy, one synchronize) -- the body of controlLoop
     void controlCycle();
-    // extra wbc_step flags for controlCycle (e.g. WBC_FUSED: one kernel per cycle instead of two)
+    // extra wbc_step flags for controlCycle (e.g. WBC_FUSED: the one-robot-per-wave kernel)
     void setStepFlags(uint32_t flags) { stepFlags_ = flags; }
 
     // ROS-free control loop (cpp:637-676): setInitialState, then per cycle
@@ -189,9 +189,10 @@ private:
     int footContacts_[numberOfLegs] = {1, 1, 1, 1};
     bool isSwitchingFootState_ = false;
 
-    // one robot: the fused kernel (one launch, no problem hand-off) measured 43.6 us per cycle
-    // against 47.2 us for the split pair (profiles/r01/s2_cycle/)
-    uint32_t stepFlags_ = WBC_FUSED;
+    // one robot: the default step (one launch, the 12-variable form with its hotstart) measured
+    // 41.2 us per cycle against 44.5 us for WBC_FUSED (one robot per wave, the 24-variable form;
+    // profiles/r03/c/b1_default.log, b1_fused.log)
+    uint32_t stepFlags_ = 0;
     int qpStatus_ = WBC_QP_OK;
     int qpIters_ = 0;
     std::array<double, numberOfJoints> tau_{};

@@ -210,7 +210,7 @@ int main(int argc, char** argv) {
             return run_stance(argc > 2 ? std::atol(argv[2]) : 1000, argc > 3 ? std::atof(argv[3]) : 0.0,
                               (argc > 4 && std::string(argv[4]) == "fused") ? WBC_FUSED
                               : (argc > 4 && std::string(argv[4]) == "split") ? WBC_SPLIT
-                              : (argc > 4 && std::string(argv[4]) == "default") ? 0u : WBC_FUSED);
+                              : 0u);  // "default" or nothing: the default step
         if (mode == "replay" && argc > 3) return run_replay(argv[2], argv[3]);
         if (mode == "run") return run_node(argc > 2 ? std::atol(argv[2]) : 200);
         std::fprintf(stderr, "usage: %s stance [cycles] [rate_hz] [fused|split|default] | run [cycles] | replay <in.bin> <out.bin>\n",
