@@ -1521,13 +1521,6 @@ __device__ bool reduce_general([[maybe_unused]] const KernelArgs& ka, [[maybe_un
 // updated with every step (no recovery pass).  Cold start only: the engine uses it for stateless
 // all-stance steps.
 // ---------------------------------------------------------------------------------------
-// min over each 16-lane DPP row of a value tagged with a 6-bit index (as wave_argmin_lane: ties to
-// the lowest index); returns the index, uniform over the row
-__device__ __forceinline__ double tag6(double v, int idx) {
-    const int hi = __double2hiint(v);
-    const int tag = (hi < 0) ? (63 - idx) : idx;
-    return __hiloint2double(hi, (__double2loint(v) & ~63) | tag);
-}
 // v_min_f64 without fmin's quieting of its DPP-moved operand (a v_max_f64 x, x per step): the
 // values reduced here are never NaN (1e300 marks "none"), and v_min_f64 is IEEE minNum anyway
 __device__ __forceinline__ double vmin_f64(double a, double b) {
@@ -1541,10 +1534,6 @@ __device__ __forceinline__ double seg16_min(double v) {
     v = vmin_f64(v, dpp_d<0x122>(v));
     v = vmin_f64(v, dpp_d<0x121>(v));
     return v;
-}
-__device__ __forceinline__ int untag6(double v) {
-    const int lo = __double2loint(v), hi = __double2hiint(v);
-    return (hi < 0) ? (63 - (lo & 63)) : (lo & 63);
 }
 // lane j of the caller's 16-lane segment (dynamic j; ds_bpermute, every lane of the segment active)
 __device__ __forceinline__ double seg_shfl(double v, int j) { return vbcast(v, ((int)threadIdx.x & ~15) + (j & 15)); }
@@ -1798,9 +1787,15 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
         const double w0 = (fon && !(ab & 1) && sp0 < -tol0) ? sp0 * in0 : 1e300;
         const double w1 = (!(ab & 2) && sp1 < -tol1) ? sp1 * in1 : 1e300;
         const double w2 = (v2 && !(ab & 4) && sp2 < -tol2) ? sp2 * in2 : 1e300;
-        const double m = seg16_min(fmin(tag6(w0, l), fmin(tag6(w1, 16 + l), tag6(w2, 32 + l))));
+        // the exact minimum, then the lowest row id holding it from three ballots (friction rows
+        // 0..15 first, then 16 + l, then 32 + l: the oracle's strict-< scan order)
+        const double m = seg16_min(vmin_f64(w0, vmin_f64(w1, w2)));
         if (!(m < 1e299)) done = true;
-        pstar = untag6(m);
+        const int sh = (int)threadIdx.x & 48;
+        const unsigned b0 = (unsigned)(__ballot(w0 == m) >> sh) & 0xFFFFu;
+        const unsigned b1 = (unsigned)(__ballot(w1 == m) >> sh) & 0xFFFFu;
+        const unsigned b2 = (unsigned)(__ballot(w2 == m) >> sh) & 0xFFFFu;
+        pstar = b0 ? __builtin_ctz(b0) : (b1 ? 16 + __builtin_ctz(b1) : 32 + __builtin_ctz(b2 | 0x10000u));
         up = 0.0;
     };
     if (!done) select();
