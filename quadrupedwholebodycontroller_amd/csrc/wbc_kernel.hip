@@ -335,6 +335,29 @@ __device__ __forceinline__ bool seg_any(bool p) {
     }
 }
 
+// v_min_f64 without fmin's quieting of its DPP-moved operand (a v_max_f64 x, x per step): the
+// values reduced here are never NaN (1e300 marks "none"), and v_min_f64 is IEEE minNum anyway
+__device__ __forceinline__ double vmin_f64(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// max(a, |b|) in one v_max_f64 (the source modifier), no quieting moves; operands never NaN here
+__device__ __forceinline__ double vmaxabs_f64(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, |%2|" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// max |S_rc| of a 6 x 6 matrix held as row r in lane r < 6 of the segment (lanes 6.. repeat row 5)
+__device__ __forceinline__ double seg6_absmax(const double (&row)[6]) {
+    double rm = 0.0;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) rm = vmaxabs_f64(rm, row[c]);
+    double m = seg_bcast<16>(rm, 0);
+#pragma unroll
+    for (int k = 1; k < 6; ++k) m = vmaxabs_f64(m, seg_bcast<16>(rm, k));
+    return m;
+}
 // One workgroup per robot: blockIdx -> robot.  (An XCD-aware remap, giving each XCD a contiguous
 // robot range so that robot-major rows sharing a cache line stay in one L2, cut HBM traffic per
 // launch 15.1 -> 11.4 MB but made the kernel 14 % slower at B = 4096, profiles/r01/variants_xcd_remap.log.)
@@ -757,17 +780,12 @@ __device__ bool stance_reduce([[maybe_unused]] const KernelArgs& ka, [[maybe_unu
     {
         const int r = lane < 6 ? lane : 5;
         double sr_[6], ir[6];
-        double smx = 0.0;
 #pragma unroll
         for (int c = 0; c < 6; ++c) {
             sr_[c] = R.S[r][c];
             ir[c] = (r == c) ? 1.0 : 0.0;
-            smx = fmax(smx, fabs(R.S[c][0]));
         }
-#pragma unroll
-        for (int c = 1; c < 6; ++c)
-#pragma unroll
-            for (int rr = 0; rr < 6; ++rr) smx = fmax(smx, fabs(R.S[rr][c]));
+        const double smx = seg6_absmax(sr_);  // max |S|: row maxima, then over the six row lanes
         double pmin = 1e300;
 #pragma unroll
         for (int kk = 0; kk < 6; ++kk) {
@@ -1273,16 +1291,12 @@ __device__ bool reduce_general([[maybe_unused]] const KernelArgs& ka, [[maybe_un
     {
         const int r = lane < 6 ? lane : 5;
         double sr_[6], ir[6];
-        double smx = 0.0;
 #pragma unroll
         for (int c = 0; c < 6; ++c) {
             sr_[c] = R.S[r][c];
             ir[c] = (r == c) ? 1.0 : 0.0;
         }
-#pragma unroll
-        for (int c = 0; c < 6; ++c)
-#pragma unroll
-            for (int rr = 0; rr < 6; ++rr) smx = fmax(smx, fabs(R.S[rr][c]));
+        const double smx = seg6_absmax(sr_);
         double pmin = 1e300;
 #pragma unroll
         for (int kk = 0; kk < 6; ++kk) {
@@ -1521,13 +1535,6 @@ __device__ bool reduce_general([[maybe_unused]] const KernelArgs& ka, [[maybe_un
 // updated with every step (no recovery pass).  Cold start only: the engine uses it for stateless
 // all-stance steps.
 // ---------------------------------------------------------------------------------------
-// v_min_f64 without fmin's quieting of its DPP-moved operand (a v_max_f64 x, x per step): the
-// values reduced here are never NaN (1e300 marks "none"), and v_min_f64 is IEEE minNum anyway
-__device__ __forceinline__ double vmin_f64(double a, double b) {
-    double r;
-    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
 __device__ __forceinline__ double seg16_min(double v) {
     v = vmin_f64(v, dpp_d<0x128>(v));
     v = vmin_f64(v, dpp_d<0x124>(v));
