@@ -4109,7 +4109,8 @@ __device__ __forceinline__ int xcd_block(int b, int n) {
 WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) {
     __shared__ UpdLds L;
     const int seg = (int)threadIdx.x / UPD_SUB, lane = (int)threadIdx.x % UPD_SUB;
-    int qp = (a.modes ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x) * UPD_RPW + seg;
+    const int blk = a.modes ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+    int qp = blk * UPD_RPW + seg;
     const bool wr = qp < a.batch;  // a padding segment recomputes the last QP, writes nothing
     if (!wr) qp = a.batch - 1;
     UST(a, qp, 30);  // kernel entry (diagnostic build)
@@ -4148,7 +4149,7 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) {
     }
     const unsigned long long fm = __ballot(fb && lane == 0);
     if (fm)
-        drain_fallbacks((const KernelArgs*)__builtin_amdgcn_kernarg_segment_ptr(), fm, (int)blockIdx.x * UPD_RPW,
+        drain_fallbacks((const KernelArgs*)__builtin_amdgcn_kernarg_segment_ptr(), fm, blk * UPD_RPW,
                         reinterpret_cast<SolveLds*>(&L));
 }
 

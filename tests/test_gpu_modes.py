@@ -59,6 +59,19 @@ def test_all_16_modes_bit_identical_to_per_row(switching):
     assert len(set(want["status"].tolist())) >= 1 and (want["status"] == 0).mean() > 0.5
 
 
+def test_modes_with_stretched_legs_bit_identical_to_per_row():
+    """A stretched (singular) leg makes the reduction unusable for the hypotheses where that leg is
+    in stance: those QPs take the update wave's general fallback from their own
+    problem record, in both paths alike."""
+    base = workloads.straight_legs(workloads.stance_cold(24, seed=25), every=2)
+    modes = list(range(16))
+    got = hypotheses(base, modes)
+    want = per_row(replicated(base, modes))
+    for k in KEYS:
+        assert np.array_equal(got[k], want[k]), k
+    assert (want["status"] == 0).mean() > 0.5
+
+
 def test_subset_of_modes_and_repeats():
     base = workloads.stance_cold(40, seed=22)
     modes = [15, 10, 5, 15, 0]  # stance, both trot pairs, a repeat, all-swing
