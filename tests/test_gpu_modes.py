@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 import wbc_np as W
-from quadrupedwholebodycontroller_amd import NO_X, STATELESS, Engine, WbcError, workloads
+from quadrupedwholebodycontroller_amd import NO_X, SPLIT, STATELESS, Engine, WbcError, workloads
 
 pytestmark = pytest.mark.gpu
 
@@ -24,12 +24,12 @@ def replicated(base, modes):
     return rep
 
 
-def per_row(inp):
+def per_row(inp, flags=STATELESS):
     B = inp["base_pose"].shape[0]
     e = Engine(B)
     e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
     e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
-    e.step(STATELESS)
+    e.step(flags)
     out = e.outputs()
     e.close()
     return out
@@ -59,14 +59,16 @@ def test_all_16_modes_bit_identical_to_per_row(switching):
     assert len(set(want["status"].tolist())) >= 1 and (want["status"] == 0).mean() > 0.5
 
 
-def test_modes_with_stretched_legs_bit_identical_to_per_row():
+@pytest.mark.parametrize("split", [False, True])
+def test_modes_with_stretched_legs_bit_identical_to_per_row(split):
     """A stretched (singular) leg makes the reduction unusable for the hypotheses where that leg is
     in stance: those QPs take the update wave's general fallback from their own
-    problem record, in both paths alike."""
+    problem record, in both paths alike; under WBC_SPLIT the split kernels' own forms."""
     base = workloads.straight_legs(workloads.stance_cold(24, seed=25), every=2)
     modes = list(range(16))
-    got = hypotheses(base, modes)
-    want = per_row(replicated(base, modes))
+    flags = STATELESS | (SPLIT if split else 0)
+    got = hypotheses(base, modes, flags)
+    want = per_row(replicated(base, modes), flags)
     for k in KEYS:
         assert np.array_equal(got[k], want[k]), k
     assert (want["status"] == 0).mean() > 0.5
