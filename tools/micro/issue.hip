@@ -42,7 +42,7 @@ int main() {
     (void)hipMalloc(&cyc, 16 * sizeof(unsigned long long));
     unsigned long long h[16];
     const char* names[] = {"fma f64", "fma f32", "mul_lo u32", "add u32", "mov_b64_dpp", "mul f64", "add f64", "max/sel i32"};
-    for (int waves = 1; waves <= 2; ++waves) {
+    for (int waves = 1; waves <= 16; waves *= 2) {
         for (int rep = 0; rep < 2; ++rep) {
             hipLaunchKernelGGL(k<0>, dim3(1), dim3(64 * waves), 0, 0, out, cyc, 0.999, 1e-3, 3);
             hipLaunchKernelGGL(k<1>, dim3(1), dim3(64 * waves), 0, 0, out, cyc, 0.999, 1e-3, 3);
@@ -54,7 +54,10 @@ int main() {
             hipLaunchKernelGGL(k<7>, dim3(1), dim3(64 * waves), 0, 0, out, cyc, 0.999, 1e-3, 3);
             (void)hipMemcpy(h, cyc, sizeof(h), hipMemcpyDeviceToHost);
         }
-        for (int i = 0; i < 8; ++i) printf("block of %d waves: %-12s %.2f cyc/instr (wave 0)\n", waves, names[i], h[i] / double(REP * N));
+        for (int i = 0; i < 8; ++i)
+            if (i == 0 || i == 3 || i == 4)
+                printf("block of %2d waves (%d per SIMD): %-12s %.2f cyc/instr (wave 0)\n", waves, (waves + 3) / 4, names[i],
+                       h[i] / double(REP * N));
     }
     return 0;
 }
