@@ -1487,7 +1487,8 @@ __device__ bool reduce_general([[maybe_unused]] const KernelArgs& ka, [[maybe_un
     {
         const int r = i;
         double my[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, t4[2] = {0.0, 0.0}, s2 = 0.0, mrow[12];
-        // Y_kk, q0_kk and B_j from their lanes (DPP broadcasts, as the H rows)
+        // Y, q0 and B from LDS (broadcast reads): kept in registers through the factorisation for
+        // DPP broadcasts instead, they pushed ~250 AGPR moves into this stage
 #pragma unroll
         for (int kk = 0; kk < 12; ++kk) {
             const double mk = P.Mbj[r * 12 + kk];
@@ -1495,8 +1496,8 @@ __device__ bool reduce_general([[maybe_unused]] const KernelArgs& ka, [[maybe_un
             const double jc = stk ? P.Jbj[kk * 12 + r] : 0.0;
             mrow[kk] = stk ? jc : -mk;  // the slot's own term of Nt[r][kk]
 #pragma unroll
-            for (int c = 0; c < 6; ++c) my[c] = fma(mk, seg_bcast<16>(yi[c], kk), my[c]);
-            t4[kk & 1] = fma(mk, seg_bcast<16>(q, kk), t4[kk & 1]);
+            for (int c = 0; c < 6; ++c) my[c] = fma(mk, R.Y[kk][c], my[c]);
+            t4[kk & 1] = fma(mk, R.q0[kk], t4[kk & 1]);
             s2 = fma(mk, mk, fma(jc, jc, s2));
         }
         double nt[12];
@@ -1504,7 +1505,7 @@ __device__ bool reduce_general([[maybe_unused]] const KernelArgs& ka, [[maybe_un
         for (int j = 0; j < 12; ++j) {
             double t = mrow[j];
 #pragma unroll
-            for (int c = 0; c < 6; ++c) t = fma(-my[c], seg_bcast<16>(Bi[c], j), t);
+            for (int c = 0; c < 6; ++c) t = fma(-my[c], V.Bt[j * 6 + c], t);
             nt[j] = t;
         }
         const double t0v = P.bbj[r] + (t4[0] + t4[1]);
