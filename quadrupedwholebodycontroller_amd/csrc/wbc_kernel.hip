@@ -87,6 +87,10 @@ struct UpdScratch {
 // Two placements: the four-contact stance form (stance_reduce, stateless all-stance waves) and
 // the general form of every contact mask (reduce_general, §4.8), whose torque map overwrites the
 // problem's Jbar joint block and which keeps the maps back to the 42 variables for the outputs.
+// friction normals, compact: face rr's row for leg l is 12 doubles from FRIC_ROW(4 l + rr) of a
+// 21-double band per face, [9 zeros | -D[rr] (3) | 9 zeros]: the row starting 9 - 3 l doubles into
+// the band has -D[rr] at 3 l .. 3 l + 2 and zeros elsewhere (84 doubles instead of 16 x 12)
+#define FRIC_ROW(p) (((p) & 3) * 21 + 9 - 3 * ((p) >> 2))
 struct St16 {
     double* Nt;    // [12][12] torque map rows: stance ja .. A (204 doubles); general P.Jbj
     double* Y;     // [12][6]  stance in; general sr.Y
@@ -100,7 +104,7 @@ struct St16 {
     double* Vt;    // [12][6]  leg row i: its coupling v_i to phi (in)
     double* rho0;  // [12]     leg row i at z = 0 (in + 72)
     double* J0;    // [12][12] copy of the initial J rows for a rejected hotstart (P.Mbj)
-    const double* fric;  // [16][12] the friction faces' normals (the workgroup's shared table)
+    const double* fric;  // friction normals, the workgroup's shared table (FRIC_ROW: row of face p)
     __device__ St16(UpdScratch& s, const double* fr)
         : Nt(&s.ja[0][0]), Y(&s.in[0]), t0(&s.in[72]), q0(&s.sc[0][0]), nsel(&s.sc[6][0]), col(&s.KA[0][0]),
           f(&s.cen[0]), Bt(nullptr), Vt(nullptr), rho0(nullptr), J0(nullptr), fric(fr) {}
@@ -1825,7 +1829,7 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
             {
                 const bool frc = pstar < 16;
                 const int tq = pstar - 16;
-                const double* nrow = frc ? &V.fric[pstar * 12] : &V.Nt[(tq >> 1) * 12];
+                const double* nrow = frc ? &V.fric[FRIC_ROW(pstar)] : &V.Nt[(tq >> 1) * 12];
                 double a4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
                 for (int k = 0; k < N; ++k) a4[k & 3] = fma(jc[k], nrow[k], a4[k & 3]);
@@ -2045,9 +2049,9 @@ __device__ __forceinline__ void load_inputs(const KernelArgs& a, int rb, int lan
     }
 }
 
-template <int SUB, bool SOLVE = false>
+template <int SUB, bool SOLVE = false, typename Model = wbc_model>
 __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int lane, bool wr, UpdScratch& s, Prob& P,
-                             Presolve* pre, const wbc_model& md, const double* fric = nullptr,
+                             Presolve* pre, const Model& md, const double* fric = nullptr,
                              const double* vin = nullptr) {
     const wbc_params& pr = a.pv;
     const bool switching = a.switching[rb] != 0;
@@ -2132,7 +2136,7 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
     {
         const int l4 = (lane >> 2) & 3, k4 = lane & 3, kk = k4 < 3 ? k4 : 2, j = 3 * l4 + kk;
         const bool base = (k4 == 3);
-        const wbc_link& lk = md.link[l4][kk];
+        const auto& lk = md.link[l4][kk];
         const double m1 = (k4 >= 1 && !base) ? 1.0 : 0.0, m2 = (k4 >= 2 && !base) ? 1.0 : 0.0;
         auto ror1 = [](double v) { return dpp_d<0x121>(v); };
         auto ror2 = [](double v) { return dpp_d<0x122>(v); };
@@ -2227,7 +2231,7 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
             const double* Il;
             if (lane == 0) { mb = md.base_mass; com = md.base_com; Il = md.base_inertia; }
             else {
-                const wbc_link& lk = md.link[(lane - 1) / 3][(lane - 1) % 3];
+                const auto& lk = md.link[(lane - 1) / 3][(lane - 1) % 3];
                 mb = lk.mass; com = lk.com; Il = lk.inertia;
             }
             double R[9], o[3], w[3], al[3], ao[3], vo[3], rel[3], t[3], u[3];
@@ -3971,9 +3975,43 @@ __device__ void solve_stance(const KernelArgs& a, int rb, const Prob* Pg, const 
 #define WBC_UPDATE_KERNEL_ATTR \
     __global__ __attribute__((amdgpu_flat_work_group_size(64, 64), amdgpu_waves_per_eu(1)))
 constexpr int UPD_SUB = 16, UPD_RPW = 64 / UPD_SUB;
+// LDS copy of wbc_model with each link record padded to 29 doubles: at the API's 28 (224 B) lanes
+// j and j + 8 of a segment read the same banks for every field of their links
+struct LdsLink {
+    double R[9], p[3], axis[3], mass, com[3], inertia[9], pad_;
+};
+static_assert(offsetof(LdsLink, pad_) == sizeof(wbc_link), "LdsLink mirrors wbc_link");
+struct LdsModel {
+    double base_mass, base_com[3], base_inertia[9];
+    LdsLink link[WBC_NUM_LEGS][3];
+    double foot[WBC_NUM_LEGS][3];
+    double total_mass;
+};
+// wbc_model -> LdsModel, element e of the destination from the source (pad entries zero)
+__device__ __forceinline__ void stage_model(LdsModel* dst, const wbc_model* src, int t) {
+    constexpr int N = (int)(sizeof(LdsModel) / 8), NB = 13, NL = 12 * 29;
+    const double* s = reinterpret_cast<const double*>(src);
+    double* d = reinterpret_cast<double*>(dst);
+    constexpr int IT = (N + 63) / 64;
+    double v[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int e = t + 64 * it < N ? t + 64 * it : N - 1;
+        const int li = e - NB, lk = li % 29;
+        const int se = e < NB ? e : (e < NB + NL ? NB + (li / 29) * 28 + (lk < 28 ? lk : 0) : e - 12);
+        const double x = s[se];
+        v[it] = (e >= NB && e < NB + NL && lk == 28) ? 0.0 : x;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int e = t + 64 * it < N ? t + 64 * it : N - 1;
+        d[e] = v[it];
+    }
+}
 struct UpdLds {
-    wbc_model model;  // staged once per wave: the kinematic chain reads it at lane-varying addresses
-    double fric[16][12];  // normals of the 16 friction faces (face 4 l + rr: -D[rr] on leg l's slot)
+    LdsModel model;   // staged once per wave: the kinematic chain reads it at lane-varying addresses
+    double fric[4 * 21];
     Prob prob[UPD_RPW];
     UpdScratch u[UPD_RPW];
 };
@@ -4047,8 +4085,7 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_kernel(KernelArgs a) {
     int rb = (int)blockIdx.x * UPD_RPW + seg;
     const bool wr = rb < a.batch;  // a padding segment recomputes the last robot, writes nothing
     if (!wr) rb = a.batch - 1;
-    stage_to_lds<(int)(sizeof(wbc_model) / 8)>(reinterpret_cast<double*>(&L.model),
-                                                reinterpret_cast<const double*>(a.model), (int)threadIdx.x);
+    stage_model(&L.model, a.model, (int)threadIdx.x);
     lds_sync();
     // work row: [Prob | Presolve]; the Presolve record is stored by update_phase itself
     Presolve* pre = reinterpret_cast<Presolve*>(a.work + (size_t)rb * WORK_LEN + PROB_LEN);
@@ -4121,18 +4158,17 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) {
     // the robot's inputs (HBM) are requested before the model staging waits for its own loads
     double vin[(91 + UPD_SUB - 1) / UPD_SUB];
     load_inputs<UPD_SUB>(a, row, lane, vin);
-    stage_to_lds<(int)(sizeof(wbc_model) / 8)>(reinterpret_cast<double*>(&L.model),
-                                                reinterpret_cast<const double*>(a.model), (int)threadIdx.x);
+    stage_model(&L.model, a.model, (int)threadIdx.x);
 #pragma unroll
-    for (int e = (int)threadIdx.x; e < 192; e += 64) {
-        const int p = e / 12, k = e % 12, rr = p & 3, r = k % 3;
-        const double fv = (r == 0) ? ((rr == 0) ? -1.0 : (rr == 1 ? 1.0 : 0.0))
-                        : (r == 1) ? ((rr == 2) ? -1.0 : (rr == 3 ? 1.0 : 0.0)) : a.pv.friction;
-        L.fric[p][k] = (k / 3 == (p >> 2)) ? fv : 0.0;
+    for (int e = (int)threadIdx.x; e < 84; e += 64) {
+        const int rr = e / 21, k = e % 21 - 9;  // k = 0..2: the band's nonzero part
+        const double fv = (k == 0) ? ((rr == 0) ? -1.0 : (rr == 1 ? 1.0 : 0.0))
+                        : (k == 1) ? ((rr == 2) ? -1.0 : (rr == 3 ? 1.0 : 0.0)) : a.pv.friction;
+        L.fric[e] = (k >= 0 && k < 3) ? fv : 0.0;
     }
     lds_sync();
     const bool solved = update_phase<UPD_SUB, true>(a, row, qp, kap, lane, wr, L.u[seg], L.prob[seg], nullptr, L.model,
-                                                    &L.fric[0][0], vin);
+                                                    &L.fric[0], vin);
     // a QP whose reduction was not usable: its problem goes to work row qp, and the wave solves it
     // with the general 24-variable method right here (drain_fallbacks, the rare path; the wave's
     // LDS is reused once the four segments are done)
