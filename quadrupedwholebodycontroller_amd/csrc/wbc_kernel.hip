@@ -61,11 +61,13 @@ struct UpdScratch {
         struct {            // four-contact stance elimination (stance_reduce), before the factorisation
             double W[12][6];    // rows of Jblk^-1 E
             double w[12];       // Jblk^-1 e
-            double S[6][8];     // [I - K W | K w], then the rows of H^ = I + Mb^-2 + Mb^-1 Q Mb^-1
-            double Si[6][8];    // S^-1 (rows)
+            // 6-row arrays padded to 9 columns (72 B): at 8 (64 B) rows r and r + 4, which lanes r
+            // and r + 4 access together, share LDS banks
+            double S[6][9];     // [I - K W | K w], then the rows of H^ = I + Mb^-2 + Mb^-1 Q Mb^-1
+            double Si[6][9];    // S^-1 (rows)
             double Y[12][6];    // W S^-1
             double q0[12];
-            double Q[6][8];     // [Y^T Y | Y^T q0]
+            double Q[6][9];     // [Y^T Y | Y^T q0]
         } sr;
     };
     double ja[12][3];       // joint axis (world)
@@ -91,6 +93,12 @@ struct UpdScratch {
 // 21-double band per face, [9 zeros | -D[rr] (3) | 9 zeros]: the row starting 9 - 3 l doubles into
 // the band has -D[rr] at 3 l .. 3 l + 2 and zeros elsewhere (84 doubles instead of 16 x 12)
 #define FRIC_ROW(p) (((p) & 3) * 21 + 9 - 3 * ((p) >> 2))
+// row stride of the J mirror (over ps.L / ps.ild of the update scratch): 14 doubles (112 B) keeps
+// rows 16-byte aligned for the b128 stores and puts no two of the 12 row lanes on the same banks
+// (at 12 doubles, 96 B, rows r and r + 8 share them); 12 x 14 ends before ps.xs
+constexpr int JMS = 14;
+static_assert(11 * JMS + 12 <= (int)((offsetof(UpdScratch, ps) + offsetof(decltype(UpdScratch::ps), xs) -
+                                      offsetof(UpdScratch, ps)) / 8), "J mirror ends before ps.xs");
 struct St16 {
     double* Nt;    // [12][12] torque map rows: stance ja .. A (204 doubles); general P.Jbj
     double* Y;     // [12][6]  stance in; general sr.Y
@@ -655,14 +663,14 @@ __device__ bool factor12_rows(double (&hrow)[12], double gsv, int lane, double* 
     }
     if (lane < 12) {
 #pragma unroll
-        for (int j = 0; j < 12; j += 2) *reinterpret_cast<double2*>(&Jm[lane * 12 + j]) = make_double2(m[j], m[j + 1]);
+        for (int j = 0; j < 12; j += 2) *reinterpret_cast<double2*>(&Jm[lane * JMS + j]) = make_double2(m[j], m[j + 1]);
     }
     lds_sync();
     // z = J0^T g (lane i: column i of the mirror . g), x0_l = -(J0 row l) . z
     const int i = lane < 12 ? lane : 0;
     double z4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int k = 0; k < 12; ++k) z4[k & 3] = fma(Jm[k * 12 + i], seg_bcast<16>(gsv, k), z4[k & 3]);
+    for (int k = 0; k < 12; ++k) z4[k & 3] = fma(Jm[k * JMS + i], seg_bcast<16>(gsv, k), z4[k & 3]);
     const double zi = (z4[0] + z4[1]) + (z4[2] + z4[3]);
     double x4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -1192,7 +1200,7 @@ __device__ bool rank6_factor(const Prob& P, UpdScratch& s, double gsv, int lane)
     if (lane < 12) {
         double* Jl = &s.ps.L[0][0];
 #pragma unroll
-        for (int j = 0; j < 12; j += 2) *reinterpret_cast<double2*>(&Jl[i * 12 + j]) = make_double2(J0[j], J0[j + 1]);
+        for (int j = 0; j < 12; j += 2) *reinterpret_cast<double2*>(&Jl[i * JMS + j]) = make_double2(J0[j], J0[j + 1]);
         s.ps.xs[i] = -f0;
     }
     lds_sync();
@@ -1611,13 +1619,13 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
     // J = L^-T (row l of J = column l of M in lane l < 12), the primal x = x0 (x_l in lane l)
     double Jr[N];
 #pragma unroll
-    for (int j = 0; j < N; ++j) Jr[j] = (l < N) ? (ROWS ? Jl[i * 12 + j] : Jl[j * 12 + i]) : 0.0;
+    for (int j = 0; j < N; ++j) Jr[j] = (l < N) ? (ROWS ? Jl[i * JMS + j] : Jl[j * 12 + i]) : 0.0;
     double x = (l < N) ? s.ps.xs[i] : 0.0;
     lds_sync();  // every lane has read M before the mirror overwrites it
     auto mirror = [&]() {
         if (l < N) {
 #pragma unroll
-            for (int j = 0; j < N; j += 2) *reinterpret_cast<double2*>(&Jl[i * 12 + j]) = make_double2(Jr[j], Jr[j + 1]);
+            for (int j = 0; j < N; j += 2) *reinterpret_cast<double2*>(&Jl[i * JMS + j]) = make_double2(Jr[j], Jr[j + 1]);
         }
         lds_sync();
     };
@@ -1658,7 +1666,7 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
         // d[pos] and J[l][pos] (needed only by the Householder add, so their LDS latency is off
         // the chain): from lane pos of the segment and from the J mirror
         dq = seg_shfl(dj, pos);  // lane 12.. holds 0
-        jq = (l >= N || pos >= N) ? 0.0 : Jl[i * 12 + (pos < N ? pos : 0)];
+        jq = (l >= N || pos >= N) ? 0.0 : Jl[i * JMS + (pos < N ? pos : 0)];
         {
             double acc[4] = {0.0, 0.0, 0.0, 0.0}, zz[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -1732,7 +1740,7 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
                     const int ol = p & 15, js = p >> 4, pos = q;
                     double jc[N];
 #pragma unroll
-                    for (int k = 0; k < N; ++k) jc[k] = Jl[k * 12 + i];
+                    for (int k = 0; k < N; ++k) jc[k] = Jl[k * JMS + i];
                     if (l == ol) {
 #pragma unroll
                         for (int k = 0; k < N; ++k) V.col[k] = sel3d(js, n0[k], n1[k], n2[k]);
@@ -1817,7 +1825,7 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
         // column i of J from the mirror, issued first so that its LDS latency is off the chain
         double jc[N];
 #pragma unroll
-        for (int k = 0; k < N; ++k) jc[k] = Jl[k * 12 + i];
+        for (int k = 0; k < N; ++k) jc[k] = Jl[k * JMS + i];
         if (!done && ++iters > max_wsr) { status = WBC_QP_MAX_ITER; iters = max_wsr; done = true; }
         if (!done) {
             const int pos = q, ol = pstar & 15, js = pstar >> 4;
