@@ -1023,21 +1023,22 @@ __device__ bool rank6_factor(const Prob& P, UpdScratch& s, double gsv, int lane)
     for (int l = 0; l < 4; ++l)
 #pragma unroll
         for (int c = 0; c < 3; ++c) { dl[l][c] = P.d[3 * l + c]; D[c] += dl[l][c]; }
+    // M22 = sum_l (|d_l|^2 I - d_l d_l^T) + (D D^T - |D|^2 I) / 4, its six distinct entries: the
+    // diagonal (a; b, c the other two axes) sum_l (d_lb^2 + d_lc^2) - (D_b^2 + D_c^2) / 4, the
+    // off-diagonal D_a D_b / 4 - sum_l d_la d_lb
     double M22[3][3];
-    {
-        const double DD = D[0] * D[0] + D[1] * D[1] + D[2] * D[2];
 #pragma unroll
-        for (int a = 0; a < 3; ++a)
-#pragma unroll
-            for (int b = 0; b < 3; ++b) M22[a][b] = 0.25 * (D[a] * D[b] - (a == b ? DD : 0.0));
+    for (int a = 0; a < 3; ++a) {
+        const int b = (a + 1) % 3, c = (a + 2) % 3;
+        double t = -0.25 * fma(D[b], D[b], D[c] * D[c]);
+        double o = 0.25 * D[a] * D[b];
 #pragma unroll
         for (int l = 0; l < 4; ++l) {
-            const double dd = dl[l][0] * dl[l][0] + dl[l][1] * dl[l][1] + dl[l][2] * dl[l][2];
-#pragma unroll
-            for (int a = 0; a < 3; ++a)
-#pragma unroll
-                for (int b = 0; b < 3; ++b) M22[a][b] += (a == b ? dd : 0.0) - dl[l][a] * dl[l][b];
+            t = fma(dl[l][b], dl[l][b], fma(dl[l][c], dl[l][c], t));
+            o = fma(-dl[l][a], dl[l][b], o);
         }
+        M22[a][a] = t;
+        M22[a][b] = M22[b][a] = o;
     }
     // L22 = chol(M22), its reciprocal diagonal
     const double sc = fmax(M22[0][0], fmax(M22[1][1], M22[2][2]));
@@ -1050,39 +1051,52 @@ __device__ bool rank6_factor(const Prob& P, UpdScratch& s, double gsv, int lane)
     const bool ok = p0 > 1e-10 * sc && p1 > 1e-10 * sc && p2 > 1e-10 * sc;
     const double L22[3][3] = {{l00, 0.0, 0.0}, {l10, l11, 0.0}, {l20, l21, l22}};
     const double SD[3][3] = {{0.0, -D[2], D[1]}, {D[2], 0.0, -D[0]}, {-D[1], D[0], 0.0}};  // S(D)
-    // X = Ĥ L_G, B = L_Gᵀ X (lower triangle), C6 = I + B
-    double X[6][6];
-#pragma unroll
-    for (int r = 0; r < 6; ++r) {
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            double t = 2.0 * Hh[r][c];
-#pragma unroll
-            for (int m = 0; m < 3; ++m) t = fma(0.5 * Hh[r][3 + m], SD[m][c], t);
-            X[r][c] = t;
-            double u = 0.0;
-#pragma unroll
-            for (int m = c; m < 3; ++m) u = fma(Hh[r][3 + m], L22[m][c], u);
-            X[r][3 + c] = u;
-        }
-    }
+    // C6 = I + L_Gᵀ Ĥ L_G, one column per lane: lane cc < 6 forms column cc of X = Ĥ L_G (6 x 6
+    // products with its column of L_G) and then column cc of C6 (L_Gᵀ's entries are uniform), and
+    // the lower triangle goes to every lane of the segment by DPP (the 6 x 6 algebra in every lane
+    // was ~250 instructions, the lane-parallel form ~90)
     double C[6][6];
+    {
+        const int cc = lane < 6 ? lane : 5;
+        const bool lin = cc < 3;
+        const int c3 = lin ? cc : cc - 3;
+        // column cc of L_G = [[2I, 0], [S(D)/2, L22]]
+        double gcol[6];
 #pragma unroll
-    for (int a = 0; a < 6; ++a) {
+        for (int k = 0; k < 3; ++k) gcol[k] = (k == cc) ? 2.0 : 0.0;
 #pragma unroll
-        for (int c = 0; c <= a; ++c) {
+        for (int m = 0; m < 3; ++m)
+            gcol[3 + m] = lin ? 0.5 * sel3d(c3, SD[m][0], SD[m][1], SD[m][2]) : sel3d(c3, L22[m][0], L22[m][1], L22[m][2]);
+        double Xc[6];
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+            double t0 = Hh[r][0] * gcol[0], t1 = Hh[r][3] * gcol[3];
+            t0 = fma(Hh[r][1], gcol[1], t0);
+            t1 = fma(Hh[r][4], gcol[4], t1);
+            t0 = fma(Hh[r][2], gcol[2], t0);
+            t1 = fma(Hh[r][5], gcol[5], t1);
+            Xc[r] = t0 + t1;
+        }
+        double Cc[6];
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
             double t;
             if (a < 3) {
-                t = 2.0 * X[a][c];
+                t = 2.0 * Xc[a];
 #pragma unroll
-                for (int m = 0; m < 3; ++m) t = fma(0.5 * SD[m][a], X[3 + m][c], t);
+                for (int m = 0; m < 3; ++m)
+                    if (m != a) t = fma(0.5 * SD[m][a], Xc[3 + m], t);
             } else {
                 t = 0.0;
 #pragma unroll
-                for (int m = a - 3; m < 3; ++m) t = fma(L22[m][a - 3], X[3 + m][c], t);
+                for (int m = a - 3; m < 3; ++m) t = fma(L22[m][a - 3], Xc[3 + m], t);
             }
-            C[a][c] = t + (a == c ? 1.0 : 0.0);
+            Cc[a] = t + ((a == cc) ? 1.0 : 0.0);
         }
+#pragma unroll
+        for (int a = 0; a < 6; ++a)
+#pragma unroll
+            for (int c = 0; c <= a; ++c) C[a][c] = seg_bcast<16>(Cc[a], c);
     }
     // L6 = chol(C6) in place (lower), id = 1 / diag; Li = L6⁻¹ (lower)
     double id[6];
@@ -1145,12 +1159,18 @@ __device__ bool rank6_factor(const Prob& P, UpdScratch& s, double gsv, int lane)
     bi[2] = ai[5] * r2;
     bi[1] = (ai[4] - l21 * bi[2]) * r1;
     bi[0] = (ai[3] - l10 * bi[1] - l20 * bi[2]) * r0;
+    // b_i . p_k(u) has two nonzero terms (p_k(u) = row k of -S(u)); written out, since x * 0.0 is
+    // not folded (x may be inf)
+    const double ha[3] = {0.5 * ai[0], 0.5 * ai[1], 0.5 * ai[2]};
     double J0[12];
 #pragma unroll
     for (int j = 0; j < 12; ++j) {
-        double pv[3];
-        pk3(j % 3, ul[j / 3], pv);
-        J0[j] = ((i == j) ? 1.0 : 0.0) + 0.5 * ai[j % 3] + (bi[0] * pv[0] + bi[1] * pv[1] + bi[2] * pv[2]);
+        const double* u = ul[j / 3];
+        const int k = j % 3;
+        const double t = (k == 0) ? fma(bi[1], u[2], fma(-bi[2], u[1], ha[0]))
+                       : (k == 1) ? fma(bi[2], u[0], fma(-bi[0], u[2], ha[1]))
+                                  : fma(bi[0], u[1], fma(-bi[1], u[0], ha[2]));
+        J0[j] = (i == j) ? t + 1.0 : t;
     }
     // f0 = -J0 J0ᵀ g: Eᵀ v = [sum_l v_l, sum_l d_l x v_l]; q6 = L_G⁻¹ Eᵀ v
     auto q6_of = [&](double vv, double* q6) {
@@ -1171,6 +1191,8 @@ __device__ bool rank6_factor(const Prob& P, UpdScratch& s, double gsv, int lane)
         for (int c = 0; c < 3; ++c) rhs[c] = bot[c] - 0.5 * dq[c];
         l22solve(rhs, &q6[3]);
     };
+    // f0 = J0 (J0ᵀ g), through the factor the loop uses: the shorter g + Q((I + B)⁻¹ - I)Qᵀ g
+    // (one Eᵀ product less) leans on QᵀQ = I and moved x* by ~2e-8 relative on stress inputs
     double q6[6];
     q6_of(gsv, q6);
     double w[6];  // w = Tᵀ q6 = Li q6 - q6

@@ -16,9 +16,11 @@ def test_step_kernels_scratch_free():
     the fallback kernel (its list loop keeps the arguments live through the solve) and
     drain_fallbacks, the call in which the default step's wave solves its own fallbacks (only the
     callee touches the stack; the kernel body stays scratch-free)."""
-    waves = re.search(r"^WAVES \?= (\d+)", open(os.path.join(CSRC, "Makefile")).read(), re.M).group(1)
+    mk = open(os.path.join(CSRC, "Makefile")).read()
+    waves = re.search(r"^WAVES \?= (\d+)", mk, re.M).group(1)
+    kflags = re.search(r"^KFLAGS := (.*)$", mk, re.M).group(1).split()  # the kernel's own flags
     r = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-I", os.path.join(ROOT, "include"),
-                        "-I", CSRC, f"-DWBC_WAVES_PER_SIMD={waves}", "-S", "--offload-device-only",
+                        "-I", CSRC, f"-DWBC_WAVES_PER_SIMD={waves}", *kflags, "-S", "--offload-device-only",
                         os.path.join(CSRC, "wbc_kernel.hip"), "-o", "-"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = r.stdout.split("\n")
