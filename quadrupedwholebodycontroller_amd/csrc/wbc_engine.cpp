@@ -42,6 +42,7 @@ struct wbc_engine {
     hipStream_t stream = nullptr;
     wbc_model* d_model = nullptr;
     wbc_params* d_params = nullptr;
+    double* d_limg = nullptr;  // the step kernel's LDS image of the model + friction table (wbc_layout.h)
     wbc_params params{};  // host copy, passed by value in the kernel arguments (KernelArgs::pv)
     // owned inputs: one device block [pose | nu | qj | ref | contacts | switching] (so a host cycle
     // is one H2D copy), and the outputs one block [tau | grf | status | iters | x]
@@ -119,6 +120,7 @@ wbc::KernelArgs make_args(wbc_engine* h, uint32_t flags) {
     wbc::KernelArgs a;
     a.model = h->d_model;
     a.params = h->d_params;
+    a.limg = h->d_limg;
     a.pv = h->params;
     a.base_pose = h->in_pose;
     a.nu = h->in_nu;
@@ -247,6 +249,7 @@ int32_t wbc_create(const wbc_model* model, const wbc_params* params, int32_t bat
     }
     ALLOC(d_model, 1);
     ALLOC(d_params, 1);
+    ALLOC(d_limg, wbc::LIMG_LEN);
     if (hipMalloc(&h->d_inblk, in_block_bytes(B)) != hipSuccess || hipMalloc(&h->d_outblk, out_block_bytes(B)) != hipSuccess) {
         wbc_destroy(h);
         return fail(WBC_ERR_HIP, "hipMalloc failed: input/output blocks");
@@ -292,8 +295,11 @@ int32_t wbc_create(const wbc_model* model, const wbc_params* params, int32_t bat
     h->out_status = h->d_status;
     h->out_iters = h->d_iters;
     hipStream_t st = h->stream;
+    wbc::LdsImage limg;
+    wbc::build_lds_image(m, p.friction, limg);
     if (hipMemcpyAsync(h->d_model, &m, sizeof(m), hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(h->d_params, &p, sizeof(p), hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(h->d_limg, &limg, sizeof(limg), hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemsetAsync(h->d_pose, 0, B * WBC_POSE_LEN * sizeof(double), st) != hipSuccess ||
         hipMemsetAsync(h->d_nu, 0, B * WBC_NU_LEN * sizeof(double), st) != hipSuccess ||
         hipMemsetAsync(h->d_qj, 0, B * WBC_NUM_JOINTS * sizeof(double), st) != hipSuccess ||
@@ -321,7 +327,7 @@ int32_t wbc_destroy(wbc_engine* h) {
     // drain the engine's in-flight work before freeing (the bound stream; never the whole device,
     // which would also wait for other engines' and the caller's unrelated work)
     (void)drain(h);
-    void* ptrs[] = {h->d_model, h->d_params, h->d_inblk, h->d_outblk, h->d_mask, h->d_modes, h->d_hist, h->d_work,
+    void* ptrs[] = {h->d_model, h->d_params, h->d_limg, h->d_inblk, h->d_outblk, h->d_mask, h->d_modes, h->d_hist, h->d_work,
                     h->d_fb, h->d_dbg};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);

@@ -89,10 +89,10 @@ struct UpdScratch {
 // Two placements: the four-contact stance form (stance_reduce, stateless all-stance waves) and
 // the general form of every contact mask (reduce_general, §4.8), whose torque map overwrites the
 // problem's Jbar joint block and which keeps the maps back to the 42 variables for the outputs.
-// friction normals, compact: face rr's row for leg l is 12 doubles from FRIC_ROW(4 l + rr) of a
-// 21-double band per face, [9 zeros | -D[rr] (3) | 9 zeros]: the row starting 9 - 3 l doubles into
-// the band has -D[rr] at 3 l .. 3 l + 2 and zeros elsewhere (84 doubles instead of 16 x 12)
-#define FRIC_ROW(p) (((p) & 3) * 21 + 9 - 3 * ((p) >> 2))
+// friction normals, compact (LdsImage::fric, wbc_layout.h): face rr's row for leg l is 12 doubles
+// from FRIC_ROW(4 l + rr) of a 21-double band per face, [9 zeros | -D[rr] (3) | 9 zeros]: the row
+// starting 9 - 3 l doubles into the band has -D[rr] at 3 l .. 3 l + 2 and zeros elsewhere (84
+// doubles instead of 16 x 12)
 // row stride of the J mirror (over ps.L / ps.ild of the update scratch): 14 doubles (112 B) keeps
 // rows 16-byte aligned for the b128 stores and puts no two of the 12 row lanes on the same banks
 // (at 12 doubles, 96 B, rows r and r + 8 share them); 12 x 14 ends before ps.xs
@@ -452,6 +452,54 @@ __device__ __forceinline__ double fast_rsq(double x) {
     y = fma(y, e, y);
     e = fma(-h * y, y, 0.5);
     return fma(y, e, y);
+}
+// sin / cos of a joint angle: x = n pi/2 + r by a three-part FMA (Cody-Waite) reduction, |r| <=
+// pi/4, and fdlibm's minimax kernels on r (< 1 ulp); ~40 instructions against the library
+// sincos' ~150 (its general reduction).  |x| > 1e5 (no joint angle) takes the library call.
+__device__ __forceinline__ void joint_sincos(double x, double* sn, double* cs) {
+    const double n = __builtin_rint(x * 0.63661977236758134308);  // x * 2 / pi
+    double r = fma(-n, 1.5707963267948966, x);                      // pi/2 in three parts
+    r = fma(-n, 6.123233995736766e-17, r);
+    r = fma(-n, -1.4973849048591698e-33, r);
+    const double z = r * r;
+    const double ps = fma(z, fma(z, fma(z, fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08),
+                                        2.75573137070700676789e-06), -1.98412698298579493134e-04),
+                          8.33333333332248946124e-03);
+    const double sr = fma(z * r, fma(z, ps, -1.66666666666666324348e-01), r);
+    const double pc = fma(z, fma(z, fma(z, fma(z, fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09),
+                                               -2.75573143513906633035e-07), 2.48015872894767294178e-05),
+                                 -1.38888888888741095749e-03), 4.16666666666666019037e-02);
+    const double hz = 0.5 * z, w = 1.0 - hz;
+    const double cr = w + (((1.0 - w) - hz) + z * z * pc);
+    const int q = (int)n & 3;
+    const double s0 = (q & 1) ? cr : sr, c0 = (q & 1) ? sr : cr;
+    *sn = (q & 2) ? -s0 : s0;
+    *cs = ((q + 1) & 2) ? -c0 : c0;
+    if (fabs(x) > 1e5) sincos(x, sn, cs);
+}
+// atan2 without branches (the pose angles, eulAnglesRPY cpp:12-20): t = min / max of |y|, |x| in
+// [0, 1], atan t = atan c + atan((t - c) / (1 + c t)) with c = 0, 1/2 or 1 (|reduced| < 7/16) and
+// fdlibm's atan kernel, then the octant / quadrant fix-ups; ~2 ulp (the division by fast_rcp)
+__device__ __forceinline__ double atan2_br(double y, double x) {
+    const double ax = fabs(x), ay = fabs(y);
+    const double mx = fmax(ax, ay), mn = fmin(ax, ay);
+    const double t = (mx > 0.0) ? mn * fast_rcp(mx) : 0.0;
+    const bool c1 = t >= 0.6875, c5 = !c1 && t >= 0.4375;
+    const double c = c1 ? 1.0 : (c5 ? 0.5 : 0.0);
+    const double hi = c1 ? 7.85398163397448278999e-01 : (c5 ? 4.63647609000806093515e-01 : 0.0);
+    const double lo = c1 ? 3.06161699786838301793e-17 : (c5 ? 2.26987774529616870924e-17 : 0.0);
+    const double u = (t - c) * fast_rcp(fma(c, t, 1.0));
+    const double z = u * u, w = z * z;
+    const double s1 = z * fma(w, fma(w, fma(w, fma(w, fma(w, 1.62858201153657823623e-02, 4.97687799461593236017e-02),
+                                                    6.66107313738753120669e-02), 9.09088713343650656196e-02),
+                                     1.42857142725034663711e-01), 3.33333333333329318027e-01);
+    const double s2 = w * fma(w, fma(w, fma(w, fma(w, -3.65315727442169155270e-02, -5.83357013379057348645e-02),
+                                            -7.69187620504482999495e-02), -1.11111104054623557880e-01),
+                              -1.99999999998764832476e-01);
+    const double at = hi - ((u * (s1 + s2) - lo) - u);  // atan t
+    double r = (ay > ax) ? 1.57079632679489655800e+00 - at : at;
+    r = (x < 0.0) ? 3.14159265358979311600e+00 - r : r;
+    return (y < 0.0) ? -r : r;
 }
 __device__ __forceinline__ double sel3(const double* v, int k) { return k == 0 ? v[0] : (k == 1 ? v[1] : v[2]); }
 __device__ __forceinline__ double sel4d(int k, double a, double b, double c, double d) {
@@ -2107,7 +2155,7 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
         if (two) s.in[lane + 64] = v1;
         if (lane >= 25 && lane < 37) {  // sin / cos of the joint angle this lane loaded
             double sn, cs;
-            sincos(v0, &sn, &cs);
+            joint_sincos(v0, &sn, &cs);
             s.sc[lane - 25][0] = sn;
             s.sc[lane - 25][1] = cs;
         }
@@ -2139,7 +2187,7 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
         lds_sync();
         if (lane < 12) {
             double sn, cs;
-            sincos(s.in[25 + lane], &sn, &cs);
+            joint_sincos(s.in[25 + lane], &sn, &cs);
             s.sc[lane][0] = sn;
             s.sc[lane][1] = cs;
         }
@@ -2480,12 +2528,14 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
         zeta[0] = hp[0] * inv_m; zeta[1] = hp[1] * inv_m; zeta[2] = hp[2] * inv_m;
         mv3(Icinv, hca, &zeta[3]);
     }
-    if (lane < 3) {  // eulAnglesRPY (cpp:12-20): roll, pitch, yaw on lanes 0, 1, 2 in parallel
+    {  // eulAnglesRPY (cpp:12-20): roll, pitch, yaw on lanes 0, 1, 2 in parallel (computed by
+       // every lane, stored by three: no branch around the chain, so it interleaves with the rest)
         double RB[9];
         quat_R(s.in[3], s.in[4], s.in[5], s.in[6], RB);
         const double ya = (lane == 0) ? RB[7] : ((lane == 1) ? -RB[6] : RB[3]);
         const double xa = (lane == 0) ? RB[8] : ((lane == 1) ? sqrt(RB[7] * RB[7] + RB[8] * RB[8]) : RB[0]);
-        s.cen[CEN_POSE + 3 + lane] = atan2(ya, xa);
+        const double ang = atan2_br(ya, xa);
+        if (lane < 3) s.cen[CEN_POSE + 3 + lane] = ang;
     }
     if (lane == 0) {
         double* cen = s.cen;
@@ -4005,48 +4055,16 @@ __device__ void solve_stance(const KernelArgs& a, int rb, const Prob* Pg, const 
 #define WBC_UPDATE_KERNEL_ATTR \
     __global__ __attribute__((amdgpu_flat_work_group_size(64, 64), amdgpu_waves_per_eu(1)))
 constexpr int UPD_SUB = 16, UPD_RPW = 64 / UPD_SUB;
-// LDS copy of wbc_model with each link record padded to 29 doubles: at the API's 28 (224 B) lanes
-// j and j + 8 of a segment read the same banks for every field of their links
-struct LdsLink {
-    double R[9], p[3], axis[3], mass, com[3], inertia[9], pad_;
-};
-static_assert(offsetof(LdsLink, pad_) == sizeof(wbc_link), "LdsLink mirrors wbc_link");
-struct LdsModel {
-    double base_mass, base_com[3], base_inertia[9];
-    LdsLink link[WBC_NUM_LEGS][3];
-    double foot[WBC_NUM_LEGS][3];
-    double total_mass;
-};
-// wbc_model -> LdsModel, element e of the destination from the source (pad entries zero)
-__device__ __forceinline__ void stage_model(LdsModel* dst, const wbc_model* src, int t) {
-    constexpr int N = (int)(sizeof(LdsModel) / 8), NB = 13, NL = 12 * 29;
-    const double* s = reinterpret_cast<const double*>(src);
-    double* d = reinterpret_cast<double*>(dst);
-    constexpr int IT = (N + 63) / 64;
-    double v[IT];
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-        const int e = t + 64 * it < N ? t + 64 * it : N - 1;
-        const int li = e - NB, lk = li % 29;
-        const int se = e < NB ? e : (e < NB + NL ? NB + (li / 29) * 28 + (lk < 28 ? lk : 0) : e - 12);
-        const double x = s[se];
-        v[it] = (e >= NB && e < NB + NL && lk == 28) ? 0.0 : x;
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-        const int e = t + 64 * it < N ? t + 64 * it : N - 1;
-        d[e] = v[it];
-    }
-}
 struct UpdLds {
-    LdsModel model;   // staged once per wave: the kinematic chain reads it at lane-varying addresses
-    double fric[4 * 21];
+    LdsModel model;   // staged once per wave (LdsImage): the kinematic chain reads it at lane-varying addresses
+    double fric[FRIC_LEN];
     Prob prob[UPD_RPW];
     UpdScratch u[UPD_RPW];
 };
 // four workgroups per CU (one wave per SIMD): 160 KB of LDS
 static_assert(4 * sizeof(UpdLds) <= 160 * 1024, "update_solve LDS budget");
+static_assert(offsetof(UpdLds, fric) == offsetof(LdsImage, fric) && offsetof(UpdLds, model) == 0,
+              "UpdLds starts with the LdsImage block");
 struct SolveLds {
     Prob prob;
     QpScratch q;
@@ -4115,7 +4133,7 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_kernel(KernelArgs a) {
     int rb = (int)blockIdx.x * UPD_RPW + seg;
     const bool wr = rb < a.batch;  // a padding segment recomputes the last robot, writes nothing
     if (!wr) rb = a.batch - 1;
-    stage_model(&L.model, a.model, (int)threadIdx.x);
+    stage_to_lds<LIMG_LEN>(reinterpret_cast<double*>(&L), a.limg, (int)threadIdx.x);
     lds_sync();
     // work row: [Prob | Presolve]; the Presolve record is stored by update_phase itself
     Presolve* pre = reinterpret_cast<Presolve*>(a.work + (size_t)rb * WORK_LEN + PROB_LEN);
@@ -4188,14 +4206,8 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) {
     // the robot's inputs (HBM) are requested before the model staging waits for its own loads
     double vin[(91 + UPD_SUB - 1) / UPD_SUB];
     load_inputs<UPD_SUB>(a, row, lane, vin);
-    stage_model(&L.model, a.model, (int)threadIdx.x);
-#pragma unroll
-    for (int e = (int)threadIdx.x; e < 84; e += 64) {
-        const int rr = e / 21, k = e % 21 - 9;  // k = 0..2: the band's nonzero part
-        const double fv = (k == 0) ? ((rr == 0) ? -1.0 : (rr == 1 ? 1.0 : 0.0))
-                        : (k == 1) ? ((rr == 2) ? -1.0 : (rr == 3 ? 1.0 : 0.0)) : a.pv.friction;
-        L.fric[e] = (k >= 0 && k < 3) ? fv : 0.0;
-    }
+    // the model and friction table: the host-built LDS image (wbc_layout.h), one contiguous copy
+    stage_to_lds<LIMG_LEN>(reinterpret_cast<double*>(&L), a.limg, (int)threadIdx.x);
     lds_sync();
     const bool solved = update_phase<UPD_SUB, true>(a, row, qp, kap, lane, wr, L.u[seg], L.prob[seg], nullptr, L.model,
                                                     &L.fric[0], vin);

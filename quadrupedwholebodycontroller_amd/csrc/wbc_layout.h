@@ -70,10 +70,58 @@ static_assert(sizeof(Presolve) % 16 == 0, "Presolve must keep 16-byte alignment"
 constexpr int PRE_LEN = sizeof(Presolve) / sizeof(double);
 constexpr int WORK_LEN = PROB_LEN + PRE_LEN;  // work row: [Prob | Presolve]
 
+// The step kernel's LDS image of the model and the friction-normal table, built once on the host
+// (wbc_create) and copied into LDS by each workgroup as one contiguous block: each link record is
+// padded to 29 doubles (at the API's 28, 224 B, lanes j and j + 8 of a segment read the same LDS
+// banks for every field of their links), and the table holds face rr's normal for leg l as the 12
+// doubles from FRIC_ROW(4 l + rr) (four 21-double bands: zeros, the face's three entries, zeros).
+struct LdsLink {
+    double R[9], p[3], axis[3], mass, com[3], inertia[9], pad_;
+};
+static_assert(sizeof(LdsLink) == sizeof(wbc_link) + sizeof(double), "LdsLink mirrors wbc_link");
+struct LdsModel {
+    double base_mass, base_com[3], base_inertia[9];
+    LdsLink link[WBC_NUM_LEGS][3];
+    double foot[WBC_NUM_LEGS][3];
+    double total_mass;
+};
+constexpr int FRIC_LEN = 4 * 21;
+#define FRIC_ROW(p) (((p) & 3) * 21 + 9 - 3 * ((p) >> 2))
+struct LdsImage {
+    LdsModel model;
+    double fric[FRIC_LEN];
+};
+constexpr int LIMG_LEN = sizeof(LdsImage) / sizeof(double);
+inline void build_lds_image(const wbc_model& m, double friction, LdsImage& o) {
+    o.model.base_mass = m.base_mass;
+    for (int i = 0; i < 3; ++i) o.model.base_com[i] = m.base_com[i];
+    for (int i = 0; i < 9; ++i) o.model.base_inertia[i] = m.base_inertia[i];
+    for (int l = 0; l < WBC_NUM_LEGS; ++l)
+        for (int k = 0; k < 3; ++k) {
+            const wbc_link& s = m.link[l][k];
+            LdsLink& d = o.model.link[l][k];
+            for (int i = 0; i < 9; ++i) { d.R[i] = s.R[i]; d.inertia[i] = s.inertia[i]; }
+            for (int i = 0; i < 3; ++i) { d.p[i] = s.p[i]; d.axis[i] = s.axis[i]; d.com[i] = s.com[i]; }
+            d.mass = s.mass;
+            d.pad_ = 0.0;
+        }
+    for (int l = 0; l < WBC_NUM_LEGS; ++l)
+        for (int i = 0; i < 3; ++i) o.model.foot[l][i] = m.foot[l][i];
+    o.model.total_mass = m.total_mass;
+    // face rr of a friction pyramid: [-1, 0, mu], [1, 0, mu], [0, -1, mu], [0, 1, mu] (force space)
+    for (int e = 0; e < FRIC_LEN; ++e) {
+        const int rr = e / 21, k = e % 21 - 9;
+        const double fv = (k == 0) ? ((rr == 0) ? -1.0 : (rr == 1 ? 1.0 : 0.0))
+                        : (k == 1) ? ((rr == 2) ? -1.0 : (rr == 3 ? 1.0 : 0.0)) : friction;
+        o.fric[e] = (k >= 0 && k < 3) ? fv : 0.0;
+    }
+}
+
 // Kernel arguments (one struct, passed by value).
 struct KernelArgs {
     const wbc_model* model;
     const wbc_params* params;
+    const double* limg;  // LdsImage (model in the LDS layout + friction table), LIMG_LEN doubles
     const double* base_pose;
     const double* nu;
     const double* qj;
