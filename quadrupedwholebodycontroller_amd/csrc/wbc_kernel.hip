@@ -411,9 +411,27 @@ __device__ __forceinline__ void rot_inertia(const double* R, const double* I, do
 #pragma unroll
         for (int j = 0; j < 3; ++j) o[3 * i + j] = t[3 * i] * R[3 * j] + t[3 * i + 1] * R[3 * j + 1] + t[3 * i + 2] * R[3 * j + 2];
 }
+// Reciprocal and reciprocal square root: the hardware estimate (v_rcp_f64 / v_rsq_f64) plus two
+// Newton steps (~1 ulp).  They replace IEEE division / sqrt sequences on the solver's sequential
+// chains (Cholesky pivots, substitutions, Householder scalars), where latency is the cost.
+__device__ __forceinline__ double fast_rcp(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-x, r, 1.0);
+    return fma(r, e, r);
+}
+__device__ __forceinline__ double fast_rsq(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    const double h = 0.5 * x;
+    double e = fma(-h * y, y, 0.5);
+    y = fma(y, e, y);
+    e = fma(-h * y, y, 0.5);
+    return fma(y, e, y);
+}
 __device__ __forceinline__ void inv3(const double* A, double* o) {
     double c00 = A[4] * A[8] - A[5] * A[7], c01 = A[5] * A[6] - A[3] * A[8], c02 = A[3] * A[7] - A[4] * A[6];
-    double id = 1.0 / (A[0] * c00 + A[1] * c01 + A[2] * c02);
+    double id = fast_rcp(A[0] * c00 + A[1] * c01 + A[2] * c02);
     o[0] = c00 * id; o[1] = (A[2] * A[7] - A[1] * A[8]) * id; o[2] = (A[1] * A[5] - A[2] * A[4]) * id;
     o[3] = c01 * id; o[4] = (A[0] * A[8] - A[2] * A[6]) * id; o[5] = (A[2] * A[3] - A[0] * A[5]) * id;
     o[6] = c02 * id; o[7] = (A[1] * A[6] - A[0] * A[7]) * id; o[8] = (A[0] * A[4] - A[1] * A[3]) * id;
@@ -434,24 +452,6 @@ __device__ __forceinline__ void quat_R(double qx, double qy, double qz, double q
     R[0] = 1 - (tyy + tzz); R[1] = txy - twz;       R[2] = txz + twy;
     R[3] = txy + twz;       R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
     R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
-}
-// Reciprocal and reciprocal square root: the hardware estimate (v_rcp_f64 / v_rsq_f64) plus two
-// Newton steps (~1 ulp).  They replace IEEE division / sqrt sequences on the solver's sequential
-// chains (Cholesky pivots, substitutions, Householder scalars), where latency is the cost.
-__device__ __forceinline__ double fast_rcp(double x) {
-    double r = __builtin_amdgcn_rcp(x);
-    double e = fma(-x, r, 1.0);
-    r = fma(r, e, r);
-    e = fma(-x, r, 1.0);
-    return fma(r, e, r);
-}
-__device__ __forceinline__ double fast_rsq(double x) {
-    double y = __builtin_amdgcn_rsq(x);
-    const double h = 0.5 * x;
-    double e = fma(-h * y, y, 0.5);
-    y = fma(y, e, y);
-    e = fma(-h * y, y, 0.5);
-    return fma(y, e, y);
 }
 // sin / cos of a joint angle: x = n pi/2 + r by a three-part FMA (Cody-Waite) reduction, |r| <=
 // pi/4, and fdlibm's minimax kernels on r (< 1 ulp); ~40 instructions against the library
@@ -1665,8 +1665,8 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
     const double tol0 = 1e-10;
     const double tol1 = 1e-10 * fmax(1.0, fabs(-pr.max_torque - sg * P.bbj[k1]));
     const double tol2 = 1e-10 * fmax(1.0, fabs(-pr.max_torque - sg * P.bbj[k2]));
-    const double in0 = 1.0 / sqrt(fmax(1.0 + pr.friction * pr.friction, 1e-300));
-    const double in1 = 1.0 / sqrt(fmax(V.nsel[k1], 1e-300)), in2 = 1.0 / sqrt(fmax(V.nsel[k2], 1e-300));
+    const double in0 = fast_rsq(fmax(1.0 + pr.friction * pr.friction, 1e-300));
+    const double in1 = fast_rsq(fmax(V.nsel[k1], 1e-300)), in2 = fast_rsq(fmax(V.nsel[k2], 1e-300));
     double sp0, sp1, sp2;
     auto slacks = [&](const double* xv) {
         double q0[4] = {0.0, 0.0, 0.0, 0.0}, q1[4] = {0.0, 0.0, 0.0, 0.0}, q2[4] = {0.0, 0.0, 0.0, 0.0};
@@ -2374,7 +2374,7 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
     for (int l = 0; l < 4; ++l)
 #pragma unroll
         for (int k = 0; k < 3; ++k) m += md.link[l][k].mass;
-    const double inv_m = 1.0 / m;
+    const double inv_m = fast_rcp(m);
 #pragma unroll
     for (int i = 0; i < 3; ++i) { c[i] *= inv_m; cd[i] *= inv_m; }
     const double r[3] = {c[0] - pB[0], c[1] - pB[1], c[2] - pB[2]};
@@ -2555,7 +2555,9 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
         for (int i = 0; i < 9; ++i) { P.Ic[i] = Ic[i]; P.Icinv[i] = Icinv[i]; }
     }
     UST(a, rb, 7);
-    const double dt = 1.0 / pr.loop_rate;
+    // finite differences over dt = 1 / loop_rate (cpp:394): times loop_rate instead of divided by
+    // dt (an IEEE division is ~10 dependent instructions; the two agree to an ulp)
+    const double rdt = pr.loop_rate;
 
     // lane = joint column j: Jbar joint column, Mbar_j column, bbar_j
     if (lane < 12) {
@@ -2596,7 +2598,7 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
         double dr[3] = {0, 0, 0};
         if (!switching) {
 #pragma unroll
-            for (int i = 0; i < 3; ++i) dr[i] = (r[i] - hR[i]) / dt;
+            for (int i = 0; i < 3; ++i) dr[i] = (r[i] - hR[i]) * rdt;
         }
 #pragma unroll
         for (int it = 0; it < NT; ++it) {
@@ -2610,8 +2612,8 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
             double Tj[6];
 #pragma unroll
             for (int rr = 0; rr < 3; ++rr) {
-                Tj[rr] = switching ? 0.0 : (s.A[j][rr] * inv_m - hMa[it][rr]) / dt;
-                Tj[3 + rr] = switching ? 0.0 : (s.KA[j][rr] - hMa[it][3 + rr]) / dt;
+                Tj[rr] = switching ? 0.0 : (s.A[j][rr] * inv_m - hMa[it][rr]) * rdt;
+                Tj[3 + rr] = switching ? 0.0 : (s.KA[j][rr] - hMa[it][3 + rr]) * rdt;
             }
             double t1[3], t2[3];
             cross3(dr, s.KA[j], t1);
@@ -2671,8 +2673,8 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
         const double kr1 = unmasked ? 1.0 : kn, ksw = unmasked ? 0.0 : kn;
         double jc_dot = 0.0, js_dot = 0.0;
         if (!switching) {
-            jc_dot = (kr1 * cur - ko * old) / dt;
-            js_dot = ((1.0 - ksw) * cur - (1.0 - ko) * old) / dt;
+            jc_dot = (kr1 * cur - ko * old) * rdt;
+            js_dot = ((1.0 - ksw) * cur - (1.0 - ko) * old) * rdt;
         }
         const double cmd = (ref[42 + i] + pr.kd_swing * (ref[30 + i] - s.vf[l][rr]) + pr.kp_swing * (ref[18 + i] - s.pf[l][rr])) *
                            (1.0 - ksw);
@@ -2690,7 +2692,7 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
         const double e = s.cen[CEN_POSE + k] - ref[k];
         P.W[k] = -kp * e - pr.kd * (s.cen[CEN_VC + k] - ref[6 + k]) - pr.ki * eint +
                  (k == 2 ? md.total_mass * pr.gravity : 0.0) + mba;
-        if (stateful && wr) H[H_EINT + k] = eint + e / pr.loop_rate;
+        if (stateful && wr) H[H_EINT + k] = eint + e * fast_rcp(pr.loop_rate);
     }
     stateful ? wsync() : lds_sync();
     if (stateful && wr) {
