@@ -1,0 +1,78 @@
+"""CPU: the step kernel's own sin / cos and atan2 (wbc_kernel.hip joint_sincos, atan2_br) against the
+C library, by compiling the kernel's source text of the two functions for the host (g++): the joint
+angles' sin / cos within 1 ulp, the pose angles' atan2 within 2 ulp (the reference computes them with
+std::sin / std::cos / std::atan2 through iDynTree and eulAnglesRPY, cpp:12-20).  The hardware
+reciprocal estimate of fast_rcp is replaced by a division on the host; its two Newton steps stay."""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNEL = os.path.join(ROOT, "quadrupedwholebodycontroller_amd", "csrc", "wbc_kernel.hip")
+
+
+def _function(src, signature):
+    i = src.index(signature)
+    depth, j = 0, src.index("{", i)
+    while True:
+        c = src[j]
+        depth += (c == "{") - (c == "}")
+        j += 1
+        if depth == 0:
+            return src[i:j]
+
+
+def test_trig_kernels_against_libm(tmp_path):
+    src = open(KERNEL).read()
+    funcs = [_function(src, s) for s in ("__device__ __forceinline__ double fast_rcp(",
+                                         "__device__ __forceinline__ void joint_sincos(",
+                                         "__device__ __forceinline__ double atan2_br(")]
+    body = "\n".join(funcs).replace("__device__ __forceinline__", "static inline")
+    body = body.replace("__builtin_amdgcn_rcp(x)", "(1.0 / x)").replace("__builtin_rint", "std::rint")
+    body = re.sub(r"sincos\(x, sn, cs\);", "{ *sn = std::sin(x); *cs = std::cos(x); }", body)
+    prog = tmp_path / "t.cpp"
+    prog.write_text(r"""
+#include <cmath>
+#include <cstdio>
+#include <random>
+using std::fma; using std::fabs; using std::fmax; using std::fmin;
+""" + body + r"""
+static double ulps(double a, double r) {
+    const double u = std::nextafter(fabs(r), INFINITY) - fabs(r);
+    return fabs(a - r) / (u > 0 ? u : 1e-300);
+}
+int main() {
+    std::mt19937_64 g(7);
+    std::uniform_real_distribution<double> q(-12.0, 12.0), v(-1.0, 1.0);
+    double es = 0, ec = 0, ea = 0;
+    for (long k = 0; k < 2000000; ++k) {
+        double x = q(g), s, c;
+        if (k < 4000) x = (k - 2000) * 0.0015707963267948966;  // multiples of pi / 2000 around 0
+        joint_sincos(x, &s, &c);
+        es = fmax(es, ulps(s, std::sin(x)));
+        ec = fmax(ec, ulps(c, std::cos(x)));
+        double y = v(g), w = v(g);
+        if (k % 5 == 0) w *= 1e-3;
+        ea = fmax(ea, ulps(atan2_br(y, w), std::atan2(y, w)));
+    }
+    double big_s, big_c;
+    joint_sincos(3.0e5, &big_s, &big_c);  // the library path beyond |x| = 1e5
+    std::printf("%.3f %.3f %.3f %d\n", es, ec, ea, big_s == std::sin(3.0e5) && big_c == std::cos(3.0e5));
+    std::printf("%.17g %.17g %.17g\n", atan2_br(0.0, -1.0), atan2_br(1.0, 0.0), atan2_br(-1.0, -1.0));
+}
+""")
+    exe = tmp_path / "t"
+    r = subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", str(prog), "-o", str(exe)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120).stdout.split("\n")
+    es, ec, ea, big = out[0].split()
+    assert float(es) <= 1.0 and float(ec) <= 1.0, (es, ec)
+    assert float(ea) <= 2.0, ea
+    assert big == "1"
+    a0, a1, a2 = (float(t) for t in out[1].split())
+    assert a0 == pytest.approx(3.141592653589793, abs=1e-15)
+    assert a1 == pytest.approx(1.5707963267948966, abs=1e-15)
+    assert a2 == pytest.approx(-2.356194490192345, abs=1e-15)
