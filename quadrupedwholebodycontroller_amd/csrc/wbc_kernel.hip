@@ -2010,18 +2010,26 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
     }
     IST_FLUSH(a, rb);
     UST(a, rb, 16);  // active-set loop
-    if (l < N) V.f[l] = x;
-    lds_sync();
     UST(a, rb, 17);  // primal
     const bool ok = (status == WBC_QP_OK);
     const bool stl = GEN ? (((kap >> (i / 3)) & 1) != 0) : true;  // slot i is a stance force
-    if (wr && l < N) {  // tau_j = t0_j - Nt_j z (cpp:565-576), grf = f (cpp:556-563)
-        double t4[4] = {0.0, 0.0, 0.0, 0.0};
+    {  // tau_j = t0_j - Nt_j z (cpp:565-576), grf = f (cpp:556-563): z by DPP from its lanes (no
+       // LDS round trip), the Nt row's reads issued alongside
+        double zb[N];
 #pragma unroll
-        for (int c = 0; c < 12; ++c) t4[c & 3] = fma(V.Nt[l * 12 + c], V.f[c], t4[c & 3]);
-        const double tv = V.t0[l] - ((t4[0] + t4[1]) + (t4[2] + t4[3]));
-        a.tau[(size_t)qp * 12 + l] = ok ? tv : 0.0;
-        a.grf[(size_t)qp * 12 + l] = (ok && stl) ? V.f[l] : 0.0;
+        for (int c = 0; c < N; ++c) zb[c] = seg_bcast<16>(x, c);
+        if (wr && l < N) {
+            double t4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int c = 0; c < 12; ++c) t4[c & 3] = fma(V.Nt[l * 12 + c], zb[c], t4[c & 3]);
+            const double tv = V.t0[l] - ((t4[0] + t4[1]) + (t4[2] + t4[3]));
+            a.tau[(size_t)qp * 12 + l] = ok ? tv : 0.0;
+            a.grf[(size_t)qp * 12 + l] = (ok && stl) ? x : 0.0;
+        }
+    }
+    if (a.x) {  // the 42-vector's maps read z from LDS
+        if (l < N) V.f[l] = x;
+        lds_sync();
     }
     if (a.x && wr) {  // x (42, cpp:534-541): a = Mb^-1 (E_S^T f) - g e_z, qdd, f, slacks
         double F[3] = {0, 0, 0}, Mm[3] = {0, 0, 0};
