@@ -120,7 +120,12 @@ struct St16 {
         : Nt(&P.Jbj[0]), Y(&s.sr.Y[0][0]), t0(&s.pf[0][0]), q0(&s.sr.q0[0]), nsel(&s.sc[6][0]), col(&s.KA[0][0]),
           f(&s.KA[0][0] + 16), Bt(&s.ja[0][0]), Vt(&s.in[0]), rho0(&s.in[72]), J0(&P.Mbj[0]), fric(fr) {}
 };
-static_assert(offsetof(UpdScratch, A) + sizeof(UpdScratch::A) - offsetof(UpdScratch, ja) >= 144 * sizeof(double), "St16 Nt");
+// row stride of Nt in the stance form: 13 doubles (26 dwords) puts the 12 row lanes of a segment on
+// distinct LDS banks (at 12, rows r, r + 4 and r + 8 share them); the general form's Nt lies over
+// P.Jbj (144 doubles, P.Mbj after it holds J0's copy) and keeps 12
+constexpr int NTS_ST = 13;
+static_assert(offsetof(UpdScratch, A) + sizeof(UpdScratch::A) - offsetof(UpdScratch, ja) >=
+              (11 * NTS_ST + 12) * sizeof(double), "St16 Nt");
 static_assert(offsetof(UpdScratch, jo) == offsetof(UpdScratch, ja) + sizeof(UpdScratch::ja), "St16 Bt");
 static_assert(offsetof(UpdScratch, vf) == offsetof(UpdScratch, pf) + sizeof(UpdScratch::pf), "St16 t0");
 static_assert(sizeof(UpdScratch::KA) >= 28 * sizeof(double), "St16 col / f");
@@ -1020,7 +1025,7 @@ __device__ bool stance_reduce([[maybe_unused]] const KernelArgs& ka, [[maybe_unu
             if (lane < 12) {
 #pragma unroll
                 for (int c = 0; c < 12; c += 2)
-                    *reinterpret_cast<double2*>(&V.Nt[j * 12 + c]) = make_double2(nt[c], nt[c + 1]);
+                    V.Nt[j * NTS_ST + c] = nt[c], V.Nt[j * NTS_ST + c + 1] = nt[c + 1];
 #pragma unroll
                 for (int c = 0; c < 6; c += 2) *reinterpret_cast<double2*>(&V.Y[j * 6 + c]) = make_double2(yi[c], yi[c + 1]);
                 V.q0[j] = R.q0[j];
@@ -1639,6 +1644,7 @@ template <bool ROWS, bool GEN>
 __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, const Prob& P, UpdScratch& s,
                         const St16& V, int kap, int status0) {
     constexpr int N = 12;
+    constexpr int NTS = GEN ? 12 : NTS_ST;  // Nt row stride
     const wbc_params& pr = a.pv;
     double* Jl = &s.ps.L[0][0];  // M = L^-1 (row-major 12 x 12) on entry, then the LDS mirror of J
     const int i = l < N ? l : 0;
@@ -1658,8 +1664,8 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
         const double fv = (r == 0) ? ((rr == 0) ? -1.0 : (rr == 1 ? 1.0 : 0.0))
                         : (r == 1) ? ((rr == 2) ? -1.0 : (rr == 3 ? 1.0 : 0.0)) : pr.friction;
         n0[m] = (m / 3 == fl) ? fv : 0.0;
-        n1[m] = -sg * V.Nt[k1 * 12 + m];
-        n2[m] = v2 ? -sg * V.Nt[k2 * 12 + m] : 0.0;
+        n1[m] = -sg * V.Nt[k1 * NTS + m];
+        n2[m] = v2 ? -sg * V.Nt[k2 * NTS + m] : 0.0;
     }
     const double bp1 = -pr.max_torque - sg * V.t0[k1], bp2 = -pr.max_torque - sg * V.t0[k2];
     const double tol0 = 1e-10;
@@ -1907,7 +1913,7 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
             {
                 const bool frc = pstar < 16;
                 const int tq = pstar - 16;
-                const double* nrow = frc ? &V.fric[FRIC_ROW(pstar)] : &V.Nt[(tq >> 1) * 12];
+                const double* nrow = frc ? &V.fric[FRIC_ROW(pstar)] : &V.Nt[(tq >> 1) * NTS];
                 double a4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
                 for (int k = 0; k < N; ++k) a4[k & 3] = fma(jc[k], nrow[k], a4[k & 3]);
@@ -1982,7 +1988,7 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
                                 nl = (i / 3 == (pl >> 2)) ? fv : 0.0;
                             } else {
                                 const int qt = pl - 16;
-                                nl = ((qt & 1) ? 1.0 : -1.0) * V.Nt[(qt >> 1) * 12 + i];
+                                nl = ((qt & 1) ? 1.0 : -1.0) * V.Nt[(qt >> 1) * NTS + i];
                             }
                             const double a0 = seg_sum<16>(l < N ? Jr[k] * nl : 0.0);
                             const double b0 = seg_sum<16>(l < N ? Jr[k + 1] * nl : 0.0);
@@ -2021,7 +2027,7 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
         if (wr && l < N) {
             double t4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int c = 0; c < 12; ++c) t4[c & 3] = fma(V.Nt[l * 12 + c], zb[c], t4[c & 3]);
+            for (int c = 0; c < 12; ++c) t4[c & 3] = fma(V.Nt[l * NTS + c], zb[c], t4[c & 3]);
             const double tv = V.t0[l] - ((t4[0] + t4[1]) + (t4[2] + t4[3]));
             a.tau[(size_t)qp * 12 + l] = ok ? tv : 0.0;
             a.grf[(size_t)qp * 12 + l] = (ok && stl) ? x : 0.0;
