@@ -28,6 +28,11 @@ HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 F_DYN, F_ASM, F_TAU, F_FACT, F_ITER = 9000, 14000, 600, 24696, 12936
 BYTES_COLD = 929          # 729 B in + 200 B out per cold solve
 BYTES_IN, BYTES_OUT = 729, 200  # per state read / per QP written (mode hypotheses share the state read)
+# configs[2] (stateful): SURVEY.md 8(d)'s 11 457 B per solve (the reference's per-robot history read and
+# written each cycle, hpp:154-161); the engine's own compact history (wbc_layout.h HistOff, 350 doubles)
+# read and written once per step: 729 B in + 200 B out + 2 x 2 800 B = 6 529 B per solve
+BYTES_TROT_SURVEY = 11457
+BYTES_TROT_ENGINE = BYTES_IN + BYTES_OUT + 2 * 350 * 8
 
 CONFIGS = {
     "stance_cold_b4096": dict(gen="stance_cold", batch=4096, seed=1, scaling="weak",
@@ -187,7 +192,7 @@ def make_engine(cfg, B, seed, device, stream):
 
     K = cfg.get("modes", 0)
     e = Engine(B, device=device)
-    e.set_stream(stream.cuda_stream)
+    e.set_stream(stream)
     if K:
         inp, modes = workloads.mode_states(B // K, seed)
         e.set_modes(modes)
@@ -208,7 +213,7 @@ def bench_trot(torch, stream, device, STATELESS, B=4096, T=400, seed=2):
     dev = {k: torch.from_numpy(np.ascontiguousarray(np.stack([s[k] for s in seq]))).to(f"cuda:{device}")
            for k in seq[0]}
     e = Engine(B, device=device)
-    e.set_stream(stream.cuda_stream)
+    e.set_stream(stream)
 
     def run(iters_out=None):
         e.reset()
@@ -234,12 +239,27 @@ def bench_trot(torch, stream, device, STATELESS, B=4096, T=400, seed=2):
     o = e.outputs()
     e.close()
     its = np.stack(its)
-    rl = roofline_of(step_flops(B * T, its) / T, ms / T)
+    tr, tr_src = committed_traffic("trot_stateful_b4096", B)
+    rl = roofline_of(step_flops(B * T, its) / T, ms / T, tr.get("step"), tr_src)
     rl["note"] = "per step (one wbc_update_solve_kernel launch): flops of the 400-step " \
                  "sequence / 400 over the sequence's HIP-event time / 400"
+    step_s = ms / T * 1e-3
+    hbm = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "achieved": B * BYTES_TROT_ENGINE / step_s / 1e9,
+           "frac": B * BYTES_TROT_ENGINE / step_s / 1e9 / HBM_PEAK_GBS,
+           "achieved_survey_bytes": B * BYTES_TROT_SURVEY / step_s / 1e9,
+           "frac_survey_bytes": B * BYTES_TROT_SURVEY / step_s / 1e9 / HBM_PEAK_GBS,
+           "traffic": tr.get("step"), "traffic_source": tr_src,
+           "traffic_achieved": (tr["step"] / step_s / 1e9) if tr.get("step") else None,
+           "note": "algorithmic bytes per solve: the engine's (729 B inputs + 200 B outputs + its 350-double "
+                   "history read and written) = %d B; SURVEY 8(d)'s (the reference's per-robot history) = %d B; "
+                   "traffic = PMC bytes per launch (profiles/*/pmc_trot_stateful_b4096.json)"
+                   % (BYTES_TROT_ENGINE, BYTES_TROT_SURVEY)}
     return dict(batch=B, steps=T, ms_total=ms, ms_per_step=ms / T, solves_per_s=B * T / (ms * 1e-3),
                 wall_solves_per_s=B * T / wall, status_counts_last=np.bincount(o["status"], minlength=4).tolist(),
                 mean_iters_last=float(o["iters"].mean()), mean_iters=float(its.mean()), roofline=rl,
+                roofline_hbm=hbm, traffic_per_step=tr.get("step"), traffic_source=tr_src,
+                algorithmic_bytes_per_step=dict(engine=float(B * BYTES_TROT_ENGINE), survey=float(B * BYTES_TROT_SURVEY)),
                 desc="BASELINE configs[2]: trot, alternating 2-contact modes, stateful history, inputs staged in HBM")
 
 
@@ -291,7 +311,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="stance_cold_b4096", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="stance_cold_b4096", choices=sorted(CONFIGS) + ["trot_stateful_b4096"],
+                    help="trot_stateful_b4096 (configs[2]) runs only the stateful trot sequence, as --extra times "
+                         "it (for tools/pmc.sh)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default=None,
                     help="weak: the config's batch per GPU; strong: the config's batch in total, sharded "
                          "(default: the config's own)")
@@ -329,8 +351,18 @@ def main():
             dist.init_process_group(backend)
 
     from quadrupedwholebodycontroller_amd import FUSED, NO_X, SPLIT, STATELESS, Engine
-    from quadrupedwholebodycontroller_amd.sharding import (StepOutputs, gather_step_outputs, shard_capacity,
-                                                           unpack_gathered)
+
+    if args.config == "trot_stateful_b4096":  # configs[2] alone: one JSON line of the trot's record
+        if world > 1:
+            log("bench.py: trot_stateful_b4096 runs on one GPU")
+            sys.exit(2)
+        stream = torch.cuda.Stream()
+        torch.cuda.set_stream(stream)
+        r = bench_trot(torch, stream, local_rank, STATELESS)
+        print(json.dumps(dict(metric="WBC QP solves/sec, configs[2] trot (stateful)", value=r["solves_per_s"],
+                              unit="solves/s", n_gpus=1, config={"workload": args.config}, trot=r)), flush=True)
+        return
+    from quadrupedwholebodycontroller_amd.sharding import StepPipeline, shard_capacity
 
     STEP_FLAGS = STATELESS | NO_X  # cold solves; outputs tau, grf, status, iters (the published ones)
 
@@ -347,7 +379,7 @@ def main():
     comm = torch.cuda.Stream() if world > 1 else None
     torch.cuda.set_stream(stream)
     e = Engine(B, device=local_rank)
-    e.set_stream(stream.cuda_stream)
+    e.set_stream(stream)
     if K:
         e.set_modes(modes)
     e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
@@ -355,43 +387,20 @@ def main():
     step = e.step_modes if K else e.step
 
     # Step outputs go straight into packed blocks (tau | status | iters) that the step's one
-    # collective gathers (sharding.gather_step_outputs).  Two blocks alternate, so that the gather of
-    # step k (on `comm`) overlaps step k + 1; step k + 2 waits for it before overwriting the block.
+    # collective gathers on `comm`, overlapped with the next step (sharding.StepPipeline, the class
+    # tests/test_gpu_pipeline.py runs on two ranks).
     cap = shard_capacity(B_total // (K or 1), world) * (K or 1) if scaling == "strong" else B
-    blocks = [StepOutputs(cap, device="cuda") for _ in range(2)]
-    gathered = [torch.empty(world * cap * 13, dtype=torch.float64, device="cuda") for _ in range(2)] \
-        if world > 1 else None
-    ev_step = [torch.cuda.Event() for _ in range(2)]
-    ev_gath = [torch.cuda.Event() for _ in range(2)]
-    used = [False, False]
-
-    def bind(slot):
-        b = blocks[slot]
-        e.bind_device_outputs(tau=b.tau.data_ptr(), status=b.status.data_ptr(), iters=b.iters.data_ptr())
-
-    def one_step(k):
-        slot = k & 1
-        if world > 1 and used[slot]:
-            stream.wait_event(ev_gath[slot])  # the gather of step k - 2 has read this block
-        bind(slot)
-        step(STEP_FLAGS)
-        if world > 1:
-            ev_step[slot].record(stream)
-            with torch.cuda.stream(comm):
-                comm.wait_event(ev_step[slot])
-                gather_step_outputs(blocks[slot], world, out=gathered[slot])
-                ev_gath[slot].record(comm)
-            used[slot] = True
+    pipe = StepPipeline(e, step, STEP_FLAGS, world, cap, stream, comm)
 
     for k in range(args.warmup):
-        one_step(k)
+        pipe.step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        one_step(args.warmup + k)
+        pipe.step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -401,16 +410,10 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    last = (args.warmup + args.steps - 1) & 1
     # whole-batch outputs of the last timed step, as every rank holds them after the gather
-    if world > 1:
-        g_tau, g_status, g_iters = unpack_gathered(gathered[last], B * world if scaling == "weak" else B_total,
-                                                   world, unit=K or 1)
-    else:
-        g_tau = blocks[last].tau[: B * 12].cpu().numpy().reshape(B, 12)
-        g_status = blocks[last].status[:B].cpu().numpy()
-        g_iters = blocks[last].iters[:B].cpu().numpy()
-    bind(0)
+    g_tau, g_status, g_iters = pipe.result(pipe.last_slot, (B * world if scaling == "weak" else B_total)
+                                           if world > 1 else B, unit=K or 1)
+    pipe.bind(0)
 
     # Kernel duration for the roofline: HIP events on the launch stream around K back-to-back
     # launches (this includes the few-us dispatch gap between launches, which rocprofv3's

@@ -114,6 +114,10 @@ enum {
 #define WBC_TIMED 16u    /* wbc_step records HIP events around its kernels (wbc_last_kernel_ms) */
 #define WBC_COLD 32u     /* stateful, but the QP starts cold (no hotstart from the previous working set) */
 #define WBC_FUSED 64u    /* wbc_step as the one-robot-per-wave kernel of the general 24-variable method */
+#define WBC_GROUP 128u   /* device-bound contact masks (wbc_bind_device_inputs): group the QPs by mask on
+                          * the stream before the step (one small kernel), as the engine does on the
+                          * host for masks it copies.  Same results either way; it pays when the masks
+                          * are mixed (waves of one mask), not when they are all equal (a trot). */
 
 /* Debug record layout (doubles per robot), written by update/step under WBC_DEBUG. */
 enum {
@@ -187,13 +191,20 @@ int32_t wbc_solve(wbc_engine* h, uint32_t flags);
 /* update + solve + torques for one control cycle.  By default one kernel, four robots per wave:
  * each robot's QP is reduced exactly to 12 variables (the swing slacks and stance equalities
  * eliminated) and solved in place, any contact mask, stateless or stateful (with
- * the hotstart); a robot whose reduction is not usable (a near-singular stance leg) is solved by
- * the general method in a second launch.  WBC_SPLIT: the update kernel then the solve kernels,
- * the problem passing through HBM (the form wbc_update + wbc_solve run); WBC_FUSED: one robot per
- * wave, the general method with the problem in LDS.  All forms return the same x, tau and status;
- * `iters` counts the working-set changes of the method that ran: the 12-variable form's friction
- * and torque rows by default, the general form's rows (the swing slack rows included, the
- * convention of a dense active set on the reference's 42 x 70 QP) under WBC_SPLIT / WBC_FUSED. */
+ * the hotstart); a robot whose reduction is not usable (a near-singular stance leg) is solved with
+ * the general 24-variable method by the same wave, inside the same launch (drain_fallbacks,
+ * DESIGN.md 4.9).  A robot's result depends only on its own inputs, mask and flags, never on its
+ * batch neighbours; the QPs are grouped by contact mask (one mask per wave: the host-copied masks'
+ * map is built when they are copied, device-bound masks' under WBC_GROUP).
+ * WBC_SPLIT: the update kernel then the solve kernels, the problem passing through HBM (the form
+ * wbc_update + wbc_solve run); WBC_FUSED: one robot per wave, the general method with the problem
+ * in LDS.  All forms return the same x and tau (to rounding) and the same status while the
+ * working-set cap does not bind.  `iters` counts the working-set changes of the method that ran:
+ * the 12-variable form's friction and torque rows by default, the general form's rows (the swing
+ * slack rows included, the convention of a dense active set on the reference's 42 x 70 QP) under
+ * WBC_SPLIT / WBC_FUSED.  WBC_QP_MAX_ITER is judged on that count against max_wsr, so near the cap
+ * the default form (fewer changes for the same QP) can return WBC_QP_OK where the split / fused
+ * forms return WBC_QP_MAX_ITER. */
 int32_t wbc_step(wbc_engine* h, uint32_t flags);
 int32_t wbc_synchronize(wbc_engine* h);
 

@@ -125,6 +125,8 @@ public:
     //   beforeCycle(iteration) [stands in for the subscriber callbacks], controlCycle() (= updateState,
     //   solveQP, computeJointTorques); stops when the QP fails (cpp:654-659) or after max_iterations.
     // rate_hz > 0 sleeps to that rate like ros::Rate; 0 runs back to back.  Returns iterations run.
+    // A direct call starts with ok() true (a requestShutdown() from an earlier loop or run() is
+    // cleared); a requestShutdown() during the loop ends it.
     long controlLoop(long max_iterations, double rate_hz = 0.0,
                      const std::function<void(long)>& beforeCycle = nullptr);
 
@@ -171,6 +173,9 @@ private:
 
     std::mutex mu_;  // callbacks vs the control cycle's snapshot
     std::atomic<bool> shutdown_{false};
+    // the loop itself; run() calls it without clearing shutdown_, so a requestShutdown() issued
+    // between run()'s start and the control thread's first cycle is not lost
+    long loop(long max_iterations, double rate_hz, const std::function<void(long)>& beforeCycle);
     double runRate_ = -1.0;  // < 0: params_.loop_rate
 
     wbc_engine* engine_ = nullptr;

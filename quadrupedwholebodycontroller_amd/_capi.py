@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("WBC_LIB", os.path.join(HERE, "libwbc_hip.so"))
 
 NUM_JOINTS, NV, NC = 12, 42, 70
 POSE_LEN, NU_LEN, REF_LEN = 7, 18, 54
-STATELESS, DEBUG, NO_X, SPLIT, TIMED, COLD, FUSED = 1, 2, 4, 8, 16, 32, 64
+STATELESS, DEBUG, NO_X, SPLIT, TIMED, COLD, FUSED, GROUP = 1, 2, 4, 8, 16, 32, 64, 128
 QP_OK, QP_MAX_ITER, QP_INFEASIBLE, QP_NUMERIC = 0, 1, 2, 3
 
 # WBC_DBG_* offsets (include/wbc.h)
@@ -150,6 +150,7 @@ class Engine:
         self.lib = load_library()
         self.batch = int(batch)
         self.n_modes = 0
+        self._stream = None  # the bound caller stream object (kept alive while bound)
         self.h = C.c_void_p()
         rc = self.lib.wbc_create(C.byref(model) if model else None, C.byref(params) if params else None,
                                  self.batch, int(device), C.byref(self.h))
@@ -161,8 +162,9 @@ class Engine:
 
     def close(self):
         if self.h:
-            self.lib.wbc_destroy(self.h)
+            self.lib.wbc_destroy(self.h)  # synchronizes the bound stream, which is still alive here
             self.h = C.c_void_p()
+        self._stream = None
 
     def __del__(self):
         try:
@@ -199,9 +201,14 @@ class Engine:
         v = [C.c_void_p(int(p)) if p else None for p in (tau, grf, x, status, iters)]
         self._check(self.lib.wbc_bind_device_outputs(self.h, *v), "wbc_bind_device_outputs")
 
-    def set_stream(self, stream_ptr: int):
-        self._check(self.lib.wbc_set_stream(self.h, C.c_void_p(int(stream_ptr)) if stream_ptr else None),
-                    "wbc_set_stream")
+    def set_stream(self, stream):
+        """Bind a caller stream: a torch.cuda.Stream (or any object with `cuda_stream`), which the engine
+        keeps referenced until it is unbound (set_stream(0 / None)) or closed, so the stream outlives
+        its binding (include/wbc.h wbc_set_stream); or a raw hipStream_t as an int, which the caller
+        must keep alive that long.  0 / None: the engine's own stream."""
+        ptr = int(getattr(stream, "cuda_stream", stream) or 0)
+        self._check(self.lib.wbc_set_stream(self.h, C.c_void_p(ptr) if ptr else None), "wbc_set_stream")
+        self._stream = stream if ptr else None
 
     # --- execution ----------------------------------------------------------------------
     def reset(self, mask=None):

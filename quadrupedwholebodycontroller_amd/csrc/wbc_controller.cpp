@@ -194,6 +194,11 @@ void WholeBodyController::terminate() {
 }
 
 long WholeBodyController::controlLoop(long max_iterations, double rate_hz, const std::function<void(long)>& beforeCycle) {
+    shutdown_.store(false);
+    return loop(max_iterations, rate_hz, beforeCycle);
+}
+
+long WholeBodyController::loop(long max_iterations, double rate_hz, const std::function<void(long)>& beforeCycle) {
     setInitialState();  // resetRobotSimState (cpp:578-605) ends in setInitialState
     const auto period = rate_hz > 0 ? std::chrono::duration<double>(1.0 / rate_hz) : std::chrono::duration<double>(0);
     auto next = std::chrono::steady_clock::now();
@@ -223,7 +228,7 @@ long WholeBodyController::run() {
     const double rate = runRate_ < 0.0 ? params_.loop_rate : runRate_;
     std::thread ctrl([&]() {
         try {
-            cycles = controlLoop(LONG_MAX, rate, loopHook);
+            cycles = loop(LONG_MAX, rate, loopHook);
         } catch (...) {
             err = std::current_exception();
         }

@@ -19,7 +19,7 @@ extern "C" hipError_t wbc_launch_solve_general(const wbc::KernelArgs* a, hipStre
 extern "C" hipError_t wbc_launch_solve_stance(const wbc::KernelArgs* a, hipStream_t st);
 extern "C" hipError_t wbc_launch_update_solve(const wbc::KernelArgs* a, hipStream_t st);
 extern "C" hipError_t wbc_launch_reset(double* hist, const uint8_t* mask, int batch, hipStream_t st);
-extern "C" int wbc_kernel_stance_elim();
+extern "C" hipError_t wbc_launch_qmap(const uint8_t* masks, int batch, int32_t* map, hipStream_t st);
 
 namespace {
 thread_local std::string g_err;
@@ -91,12 +91,22 @@ struct wbc_engine {
     double* out_x = nullptr;
     int32_t* out_status = nullptr;
     int32_t* out_iters = nullptr;
+    // the default step's wave map (KernelArgs::qmap): QPs grouped by contact mask, four to a wave.
+    // For the engine's own masks it is built on the host whenever they are copied (qmap_waves waves;
+    // 0 = every mask equal, no map needed); for device-bound masks wbc_qmap_kernel builds it on the
+    // stream before each step
+    int32_t* d_qmap = nullptr;
+    int32_t* h_qmap = nullptr;  // pinned
+    int32_t qmap_waves = 0;
+    bool qmap_host = true;  // qmap_waves / d_qmap describe d_contacts (not after a change of modes)
     bool updated = false;
     bool timed = false;    // a WBC_TIMED step has recorded ev0 / ev1
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    // last launch on a caller's stream (wbc_set_stream): the engine waits for this event, not for
-    // the stream (which the caller may destroy) or the device (other engines' and torch's work)
-    double last_ms = 0.0;
+    // wbc_cycle's captured graph (H2D, step, D2H) and what it was captured for
+    hipGraphExec_t cyc_exec = nullptr;
+    uint32_t cyc_flags = 0;
+    hipStream_t cyc_stream = nullptr;
+    bool graph_ok = true;
 };
 
 namespace {
@@ -146,7 +156,36 @@ wbc::KernelArgs make_args(wbc_engine* h, uint32_t flags) {
     a.parity = 0;
     a.fb = h->d_fb;
     a.fb_cap = h->batch;
+    a.qmap = nullptr;
+    a.nwaves = (h->batch + wbc::QMAP_SEG - 1) / wbc::QMAP_SEG;
     return a;
+}
+
+// Host wave map of the engine's own contact masks (copied on the stream; the callers synchronize
+// before the host buffer is reused)
+hipError_t upload_qmap(wbc_engine* h, const uint8_t* masks) {
+    h->qmap_waves = wbc::qmap_build(masks, h->batch, h->h_qmap);
+    h->qmap_host = true;
+#ifdef WBC_DIAG_MAP  // (A/B diagnostics only) 1: identity order through the map, 2: a fixed shuffle
+    {
+        const int B = h->batch;
+        uint64_t x = 88172645463325252ull;
+        for (int i = 0; i < B; ++i) h->h_qmap[i] = i;
+        if (WBC_DIAG_MAP == 2)
+            for (int i = B - 1; i > 0; --i) {
+                x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+                const int j = (int)(x % (uint64_t)(i + 1));
+                const int t = h->h_qmap[i]; h->h_qmap[i] = h->h_qmap[j]; h->h_qmap[j] = t;
+            }
+        for (int i = 0; i < B; ++i) h->h_qmap[i] = wbc::qmap_entry(h->h_qmap[i], masks[h->h_qmap[i]]);
+        int w = (B + 3) / 4;
+        for (int i = B; i < 4 * w; ++i) h->h_qmap[i] = ~wbc::qmap_entry(B - 1, masks[B - 1]);
+        h->qmap_waves = w;
+    }
+#endif
+    if (!h->qmap_waves) return hipSuccess;
+    return hipMemcpyAsync(h->d_qmap, h->h_qmap, (size_t)h->qmap_waves * wbc::QMAP_SEG * sizeof(int32_t),
+                          hipMemcpyHostToDevice, h->stream);
 }
 
 // wait for every launch the engine queued so far: a stream synchronize of the bound stream (its
@@ -168,7 +207,7 @@ void begin_update(wbc_engine* h, wbc::KernelArgs& a) {
     bool all = false;
     if (h->n_modes) all = h->modes_stance == h->n_modes;
     else if (h->in_contacts == h->d_contacts) all = h->n_stance_own == h->batch;
-    h->elim = all && wbc_kernel_stance_elim();
+    h->elim = all;
     // the fallback counters alternate between elimination updates only: the update with parity p
     // fills fb[p] and clears fb[p ^ 1], which only the next elimination update uses (an update
     // without the elimination neither fills nor clears a list, so it must not move the parity)
@@ -180,10 +219,33 @@ void begin_update(wbc_engine* h, wbc::KernelArgs& a) {
 
 // The default step (wbc_update_solve_kernel: every QP reduced to 12 variables and solved in the
 // update wave) solves its own fallbacks in the wave that found them (no list), so it
-// leaves the fallback list and its parity to the split path's elimination updates.
-void begin_step16(wbc_engine* h, wbc::KernelArgs& a) {
+// leaves the fallback list and its parity to the split path's elimination updates.  Its waves each
+// hold QPs of one contact mask: the wave map (the engine's own masks: built when they were copied;
+// device-bound masks: built on the stream now under WBC_GROUP), or under mode hypotheses the
+// arithmetic map.
+hipError_t begin_step16(wbc_engine* h, wbc::KernelArgs& a, uint32_t flags) {
     a.elim = 1;
     h->elim = false;  // a later wbc_solve needs its own wbc_update
+    if (a.modes) {
+        const int S = h->batch / a.modes;
+        a.nwaves = ((S + wbc::QMAP_SEG - 1) / wbc::QMAP_SEG) * a.modes;
+        return hipSuccess;
+    }
+    if (h->in_contacts == h->d_contacts && h->qmap_host) {
+#ifndef WBC_NO_QMAP  // (A/B builds only: the unmapped step)
+        if (h->qmap_waves) {
+            a.qmap = h->d_qmap;
+            a.nwaves = h->qmap_waves;
+        }
+#endif
+        return hipSuccess;
+    }
+    // device-bound masks: the map is built on the stream when the caller asks for it (WBC_GROUP);
+    // otherwise waves take four consecutive QPs (same results; a wave of mixed masks costs more)
+    if (!(flags & WBC_GROUP)) return hipSuccess;
+    a.qmap = h->d_qmap;
+    a.nwaves = wbc::qmap_capacity(h->batch) / wbc::QMAP_SEG;
+    return wbc_launch_qmap(h->in_contacts, h->batch, h->d_qmap, h->stream);
 }
 
 hipError_t launch_solves(wbc_engine* h, wbc::KernelArgs& a) {
@@ -223,6 +285,7 @@ int32_t wbc_anymal_model(wbc_model* m) {
 
 int32_t wbc_create(const wbc_model* model, const wbc_params* params, int32_t batch, int32_t device, wbc_engine** out) {
     if (!out || batch <= 0) return fail(WBC_ERR_ARG, "wbc_create: bad arguments");
+    if (batch > wbc::QMAP_MAX_BATCH) return fail(WBC_ERR_ARG, "wbc_create: batch above 2^27 - 1 (the wave map's index range)");
     *out = nullptr;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(WBC_ERR_NO_DEVICE, "no HIP device");
@@ -275,7 +338,12 @@ int32_t wbc_create(const wbc_model* model, const wbc_params* params, int32_t bat
     ALLOC(d_work, B * wbc::WORK_LEN);
     ALLOC(d_fb, 2 + B);
     ALLOC(d_dbg, B * WBC_DBG_LEN);
+    ALLOC(d_qmap, wbc::qmap_capacity(batch));
 #undef ALLOC
+    if (hipHostMalloc(&h->h_qmap, sizeof(int32_t) * wbc::qmap_capacity(batch), hipHostMallocDefault) != hipSuccess) {
+        wbc_destroy(h);
+        return fail(WBC_ERR_HIP, "hipHostMalloc failed: wave map");
+    }
     if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) {
         wbc_destroy(h);
@@ -328,11 +396,13 @@ int32_t wbc_destroy(wbc_engine* h) {
     // which would also wait for other engines' and the caller's unrelated work)
     (void)drain(h);
     void* ptrs[] = {h->d_model, h->d_params, h->d_limg, h->d_inblk, h->d_outblk, h->d_mask, h->d_modes, h->d_hist, h->d_work,
-                    h->d_fb, h->d_dbg};
+                    h->d_fb, h->d_dbg, h->d_qmap};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (h->h_in) (void)hipHostFree(h->h_in);
     if (h->h_out) (void)hipHostFree(h->h_out);
+    if (h->h_qmap) (void)hipHostFree(h->h_qmap);
+    if (h->cyc_exec) (void)hipGraphExecDestroy(h->cyc_exec);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
@@ -375,6 +445,8 @@ int32_t wbc_set_reference(wbc_engine* h, const double* ref, const uint8_t* conta
         WBC_HIP(hipMemcpyAsync(h->d_contacts, contacts, B, hipMemcpyHostToDevice, h->stream));
         h->in_contacts = h->d_contacts;
         h->n_stance_own = count_stance(contacts, B);
+        // the wave map of these masks (rows = QPs; under mode hypotheses contacts[] is not read)
+        if (!h->n_modes) WBC_HIP(upload_qmap(h, contacts));
     }
     if (switching) { WBC_HIP(hipMemcpyAsync(h->d_switching, switching, B, hipMemcpyHostToDevice, h->stream)); h->in_switching = h->d_switching; }
     WBC_HIP(hipStreamSynchronize(h->stream));
@@ -455,7 +527,7 @@ int32_t wbc_step(wbc_engine* h, uint32_t flags) {
         WBC_HIP(wbc_launch_step(&a, h->stream));  // one robot per wave, the general method
     } else {
         // default: one kernel, every QP reduced to 12 variables and solved in the update wave
-        begin_step16(h, a);
+        WBC_HIP(begin_step16(h, a, flags));
         WBC_HIP(wbc_launch_update_solve(&a, h->stream));
     }
     if (timed) {
@@ -468,6 +540,9 @@ int32_t wbc_step(wbc_engine* h, uint32_t flags) {
 
 int32_t wbc_set_modes(wbc_engine* h, int32_t n_modes, const uint8_t* modes) {
     if (!h) return fail(WBC_ERR_ARG, "null handle");
+    // contacts[] copied while modes were set hold S rows only: the engine's own masks get their
+    // wave map on the device from here on, until the next wbc_set_reference / wbc_cycle with masks
+    h->qmap_host = false;
     if (n_modes == 0) {
         h->n_modes = 0;
         return WBC_OK;
@@ -504,7 +579,7 @@ int32_t wbc_step_modes(wbc_engine* h, uint32_t flags) {
         WBC_HIP(launch_solves(h, a));
     } else {
         // default: each hypothesis reduced and solved in its own 16-lane segment
-        begin_step16(h, a);
+        WBC_HIP(begin_step16(h, a, flags));
         WBC_HIP(wbc_launch_update_solve(&a, h->stream));
     }
     if (timed) {
@@ -514,6 +589,41 @@ int32_t wbc_step_modes(wbc_engine* h, uint32_t flags) {
     h->updated = false;
     return WBC_OK;
 }
+
+}  // extern "C"
+namespace {
+// One cycle's device work on the engine stream, from the packed pinned inputs (h_in) to the packed
+// pinned outputs (h_out): one H2D copy, the wave map's copy when the masks differ, the step on the
+// engine's own input and output buffers (caller bindings are restored afterwards), one D2H copy
+// (x, last in the block, only without WBC_NO_X).
+int32_t enqueue_cycle(wbc_engine* h, uint32_t flags) {
+    const size_t B = (size_t)h->batch;
+    const size_t inb = in_block_bytes(B), outb = out_block_bytes(B), xb = B * WBC_NV * sizeof(double);
+    WBC_HIP(hipMemcpyAsync(h->d_inblk, h->h_in, inb, hipMemcpyHostToDevice, h->stream));
+    if (h->qmap_waves)
+        WBC_HIP(hipMemcpyAsync(h->d_qmap, h->h_qmap, (size_t)h->qmap_waves * wbc::QMAP_SEG * sizeof(int32_t),
+                               hipMemcpyHostToDevice, h->stream));
+    const double* const ip = h->in_pose; const double* const in = h->in_nu; const double* const iq = h->in_qj;
+    const double* const ir = h->in_ref; const uint8_t* const ic = h->in_contacts; const uint8_t* const is = h->in_switching;
+    h->in_pose = h->d_pose;
+    h->in_nu = h->d_nu;
+    h->in_qj = h->d_qj;
+    h->in_ref = h->d_ref;
+    h->in_contacts = h->d_contacts;
+    h->in_switching = h->d_switching;
+    double* const bt = h->out_tau; double* const bg = h->out_grf; double* const bx = h->out_x;
+    int32_t* const bs = h->out_status; int32_t* const bi = h->out_iters;
+    h->out_tau = h->d_tau; h->out_grf = h->d_grf; h->out_x = h->d_x; h->out_status = h->d_status; h->out_iters = h->d_iters;
+    const int32_t rc = wbc_step(h, flags);
+    h->out_tau = bt; h->out_grf = bg; h->out_x = bx; h->out_status = bs; h->out_iters = bi;
+    h->in_pose = ip; h->in_nu = in; h->in_qj = iq; h->in_ref = ir; h->in_contacts = ic; h->in_switching = is;
+    if (rc != WBC_OK) return rc;
+    WBC_HIP(hipMemcpyAsync(h->h_out, h->d_outblk, (flags & WBC_NO_X) ? outb - xb : outb, hipMemcpyDeviceToHost,
+                           h->stream));
+    return WBC_OK;
+}
+}  // namespace
+extern "C" {
 
 int32_t wbc_cycle(wbc_engine* h, const double* base_pose, const double* nu, const double* qj, const double* ref,
                   const uint8_t* contacts, const uint8_t* switching, uint32_t flags, double* tau, double* grf, double* x,
@@ -540,29 +650,46 @@ int32_t wbc_cycle(wbc_engine* h, const double* base_pose, const double* nu, cons
     hp += B * WBC_REF_LEN;
     std::memcpy(reinterpret_cast<uint8_t*>(hp), contacts, B);
     std::memcpy(reinterpret_cast<uint8_t*>(hp) + B, switching, B);
-    WBC_HIP(hipMemcpyAsync(h->d_inblk, h->h_in, inb, hipMemcpyHostToDevice, h->stream));
     h->n_stance_own = count_stance(contacts, B);  // d_contacts holds these masks from here on
-    // inputs from the engine's own block for this step only (caller bindings are restored after)
-    const double* const ip = h->in_pose; const double* const in = h->in_nu; const double* const iq = h->in_qj;
-    const double* const ir = h->in_ref; const uint8_t* const ic = h->in_contacts; const uint8_t* const is = h->in_switching;
-    h->in_pose = h->d_pose;
-    h->in_nu = h->d_nu;
-    h->in_qj = h->d_qj;
-    h->in_ref = h->d_ref;
-    h->in_contacts = h->d_contacts;
-    h->in_switching = h->d_switching;
-    // outputs into the engine's own block (caller bindings are restored afterwards)
-    double* const bt = h->out_tau; double* const bg = h->out_grf; double* const bx = h->out_x;
-    int32_t* const bs = h->out_status; int32_t* const bi = h->out_iters;
-    h->out_tau = h->d_tau; h->out_grf = h->d_grf; h->out_x = h->d_x; h->out_status = h->d_status; h->out_iters = h->d_iters;
+    h->qmap_waves = wbc::qmap_build(contacts, h->batch, h->h_qmap);  // uploaded by enqueue_cycle
+    h->qmap_host = true;
     if (!x) flags |= WBC_NO_X;
-    const int32_t rc = wbc_step(h, flags);
-    h->out_tau = bt; h->out_grf = bg; h->out_x = bx; h->out_status = bs; h->out_iters = bi;
-    h->in_pose = ip; h->in_nu = in; h->in_qj = iq; h->in_ref = ir; h->in_contacts = ic; h->in_switching = is;
-    if (rc != WBC_OK) return rc;
-    // one D2H copy (x, last in the block, only when asked for)
+    // Replayed from a captured HIP graph (H2D copy, step kernel, D2H copy: one launch call instead
+    // of three) while nothing in it changes: the same flags and stream and no wave map to upload
+    // (every mask equal, e.g. the B = 1 drop-in), not split (its update alternates fallback counters)
+    // or timed.  Otherwise, and if capture fails, enqueued eagerly.
+#ifndef WBC_NO_CYCLE_GRAPH  // (A/B builds only: the eager cycle)
+    const bool graphable = h->qmap_waves == 0 && !(flags & (WBC_TIMED | WBC_SPLIT)) && h->graph_ok;
+#else
+    const bool graphable = false;
+#endif
+    if (graphable && h->cyc_exec && (h->cyc_flags != flags || h->cyc_stream != h->stream)) {
+        (void)hipGraphExecDestroy(h->cyc_exec);
+        h->cyc_exec = nullptr;
+    }
+    if (graphable && !h->cyc_exec) {
+        hipGraph_t g = nullptr;
+        bool ok = hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal) == hipSuccess;
+        const int32_t rc = ok ? enqueue_cycle(h, flags) : WBC_OK;
+        ok = (hipStreamEndCapture(h->stream, &g) == hipSuccess) && ok && rc == WBC_OK && g;
+        ok = ok && hipGraphInstantiate(&h->cyc_exec, g, nullptr, nullptr, 0) == hipSuccess;
+        if (g) (void)hipGraphDestroy(g);
+        if (!ok) {  // e.g. a stream that cannot be captured: eager from now on
+            h->cyc_exec = nullptr;
+            h->graph_ok = false;
+            (void)hipGetLastError();
+        } else {
+            h->cyc_flags = flags;
+            h->cyc_stream = h->stream;
+        }
+    }
+    if (graphable && h->cyc_exec) {
+        WBC_HIP(hipGraphLaunch(h->cyc_exec, h->stream));
+    } else {
+        const int32_t rc = enqueue_cycle(h, flags);
+        if (rc != WBC_OK) return rc;
+    }
     const size_t xb = B * WBC_NV * sizeof(double);
-    WBC_HIP(hipMemcpyAsync(h->h_out, h->d_outblk, x ? outb : outb - xb, hipMemcpyDeviceToHost, h->stream));
     WBC_HIP(hipStreamSynchronize(h->stream));
     const double* o = static_cast<const double*>(h->h_out);
     if (tau) std::memcpy(tau, o, B * WBC_NUM_JOINTS * sizeof(double));

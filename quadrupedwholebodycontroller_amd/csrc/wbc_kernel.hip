@@ -2815,10 +2815,16 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
     // the other hypotheses factor their slot Hessian in the solve.
     if constexpr (SOLVE) {
         static_assert(SUB == 16, "the inline solve runs in 16-lane segments");
-        // stateless waves whose four robots all have mask 15: the four-contact stance form
-        // (stance_reduce + the rank-6 factor, no Hessian to factor); every other wave: the general
-        // form, per robot (its own mask, a hotstart on stateful steps)
+        // a stateless QP of mask 15: the four-contact stance form (stance_reduce + the rank-6
+        // factor, no Hessian to factor); every other QP: the general form (its own mask, a hotstart
+        // on stateful steps).  The choice is the segment's own, so a QP's result never depends on
+        // its wave-mates; the wave map (KernelArgs::qmap) gives every wave one mask, so the branch
+        // does not diverge (a mixed wave, from unmapped device-bound masks, runs both forms)
+#ifndef WBC_WAVE_FORM
+        if (!stateful && kap == 15) {
+#else  // (A/B diagnostics only: the form chosen per wave, as before the wave map)
         if (!stateful && __all(kap == 15)) {
+#endif
             double hrow[12], gsv = 0.0;
             if (stance_reduce<true>(a, rb, P, pr, lane, wr, s, hrow, gsv, nullptr) && rank6_factor(P, s, gsv, lane)) {
                 UST(a, rb, 11);
@@ -4187,7 +4193,7 @@ static_assert(sizeof(SolveLds) <= sizeof(UpdLds), "the drain reuses the update s
 // A call (the rare path stays out of the kernel's register allocation), handed the address of the
 // kernel's arguments in its kernarg segment (passing the struct would pin a stack copy to the whole
 // kernel; a callee has no kernarg pointer of its own).
-__device__ __attribute__((noinline)) void drain_fallbacks(const KernelArgs* ka, unsigned long long fm, int qp0,
+__device__ __attribute__((noinline)) void drain_fallbacks(const KernelArgs* ka, unsigned long long fm, int qp,
                                                           SolveLds* L) {
     KernelArgs f = *ka;
     f.modes = 0;
@@ -4197,7 +4203,7 @@ __device__ __attribute__((noinline)) void drain_fallbacks(const KernelArgs* ka, 
         const int seg = __builtin_ctzll(fm) / UPD_SUB;
         fm &= fm - 1ull;
         wsync();
-        solve_general_qp(f, qp0 + seg, *L);
+        solve_general_qp(f, __builtin_amdgcn_readlane(qp, seg * UPD_SUB), *L);
     }
 }
 // Workgroups are dispatched to the 8 XCDs round-robin (block b on XCD b % 8), each with its own
@@ -4211,19 +4217,48 @@ __device__ __forceinline__ int xcd_block(int b, int n) {
 WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) {
     __shared__ UpdLds L;
     const int seg = (int)threadIdx.x / UPD_SUB, lane = (int)threadIdx.x % UPD_SUB;
-    const int blk = a.modes ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
-    int qp = blk * UPD_RPW + seg;
-    const bool wr = qp < a.batch;  // a padding segment recomputes the last QP, writes nothing
-    if (!wr) qp = a.batch - 1;
-    UST(a, qp, 30);  // kernel entry (diagnostic build)
     const int K = a.modes;
-    const int row = K ? qp / K : qp;
-    const int kap = (K ? a.mode_masks[qp - row * K] : a.contacts[row]) & 15;
+    int qp, row, kap;
+    bool wr, empty = false;
+    if (K) {
+        // workgroup g K + k: states 4 g .. 4 g + 3 under mask modes[k] (one mask per wave); the K
+        // workgroups of a state group are consecutive, and xcd_block keeps them on one XCD
+        const int blk = xcd_block((int)blockIdx.x, (int)gridDim.x);
+        const int S = a.batch / K, g = blk / K, k = blk - g * K;
+        row = 4 * g + seg;
+        wr = row < S;  // a padding segment recomputes the last state, writes nothing
+        if (!wr) row = S - 1;
+        qp = row * K + k;
+        kap = a.mode_masks[k] & 15;
+    } else {
+        // the wave map groups the QPs by contact mask (KernelArgs::qmap): the workgroup's four
+        // entries as one uniform 16-byte (scalar) load
+        int e = (int)blockIdx.x * UPD_RPW + seg;
+        if (a.qmap) {
+            const int4 e4 = reinterpret_cast<const int4*>(a.qmap)[blockIdx.x];
+            e = (seg == 0) ? e4.x : (seg == 1) ? e4.y : (seg == 2) ? e4.z : e4.w;
+        }
+        if (a.qmap) {
+            empty = e == QMAP_EMPTY;
+            wr = e >= 0;
+            const int v = empty ? qmap_entry(a.batch - 1, 15) : (wr ? e : ~e);
+            qp = v >> 4;
+            kap = v & 15;
+            row = qp;
+        } else {
+            wr = e < a.batch;
+            qp = wr ? e : a.batch - 1;
+            row = qp;
+            kap = a.contacts[row] & 15;
+        }
+    }
+    UST(a, qp, 30);  // kernel entry (diagnostic build)
     // the robot's inputs (HBM) are requested before the model staging waits for its own loads
     double vin[(91 + UPD_SUB - 1) / UPD_SUB];
     load_inputs<UPD_SUB>(a, row, lane, vin);
     // the model and friction table: the host-built LDS image (wbc_layout.h), one contiguous copy
     stage_to_lds<LIMG_LEN>(reinterpret_cast<double*>(&L), a.limg, (int)threadIdx.x);
+    if (__all(empty)) return;  // the unused tail of a device-built map (uniform)
     lds_sync();
     const bool solved = update_phase<UPD_SUB, true>(a, row, qp, kap, lane, wr, L.u[seg], L.prob[seg], nullptr, L.model,
                                                     &L.fric[0], vin);
@@ -4244,7 +4279,7 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) {
     }
     const unsigned long long fm = __ballot(fb && lane == 0);
     if (fm)
-        drain_fallbacks((const KernelArgs*)__builtin_amdgcn_kernarg_segment_ptr(), fm, blk * UPD_RPW,
+        drain_fallbacks((const KernelArgs*)__builtin_amdgcn_kernarg_segment_ptr(), fm, qp,
                         reinterpret_cast<SolveLds*>(&L));
 }
 
@@ -4330,6 +4365,66 @@ void wbc_solve_stance_kernel(KernelArgs a) {
                  reinterpret_cast<const Presolve*>(prow), S);
 }
 
+// The default step's wave map for device-bound contact masks (KernelArgs::qmap, under WBC_GROUP):
+// the layout of qmap_build (wbc_layout.h qmap_plan / qmap_pos), then QMAP_EMPTY up to the capacity,
+// so the step launches qmap_capacity(B) / 4 workgroups without reading the masks back.  One
+// workgroup: thread t counts and later places robots [t C, (t + 1) C) with its own LDS column of
+// per-mask counts, the columns are scanned per mask over the threads.
+constexpr int QMAP_THREADS = 256;
+__global__ __launch_bounds__(QMAP_THREADS) void wbc_qmap_kernel(const uint8_t* masks, int B, int32_t* map, int cap) {
+    __shared__ int col[16][QMAP_THREADS];  // counts, then inclusive prefixes over the threads
+    __shared__ int tot[16], first[16];
+    __shared__ QmapPlan plan;
+    const int t = (int)threadIdx.x;
+    const int C = (B + QMAP_THREADS - 1) / QMAP_THREADS, b0 = min(t * C, B), b1 = min(b0 + C, B);
+#pragma unroll
+    for (int m = 0; m < 16; ++m) col[m][t] = 0;
+    if (t < 16) first[t] = B;
+    __syncthreads();
+    for (int b = b0; b < b1; ++b) {
+        const int m = masks[b] & 15;
+        if (col[m][t]++ == 0) atomicMin(&first[m], b);
+    }
+    __syncthreads();
+    int own[16];  // this thread's counts (the exclusive prefix is the inclusive one minus these)
+#pragma unroll
+    for (int m = 0; m < 16; ++m) own[m] = col[m][t];
+    for (int d = 1; d < QMAP_THREADS; d <<= 1) {  // Hillis-Steele, all masks per step
+        int v[16];
+#pragma unroll
+        for (int m = 0; m < 16; ++m) v[m] = (t >= d) ? col[m][t - d] : 0;
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < 16; ++m) col[m][t] += v[m];
+        __syncthreads();
+    }
+    if (t < 16) tot[t] = col[t][QMAP_THREADS - 1];
+    __syncthreads();
+    if (t == 0) {
+        int f[16];
+        for (int m = 0; m < 16; ++m) f[m] = first[m] < B ? first[m] : -1;
+        qmap_plan(tot, f, plan);
+    }
+    __syncthreads();
+    int j[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) j[m] = col[m][t] - own[m];
+    for (int b = b0; b < b1; ++b) {
+        const int m = masks[b] & 15;
+        int jm = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {  // register select (a dynamic index would go to scratch)
+            jm = (k == m) ? j[k] : jm;
+            j[k] += (k == m);
+        }
+        map[qmap_pos(plan, m, jm)] = qmap_entry(b, m);
+    }
+    const int used = 4 * plan.waves;
+    if (t < QMAP_SEG && plan.base1 && t >= plan.pad0) map[t] = plan.v0;
+    if (t >= QMAP_SEG && t < 2 * QMAP_SEG && plan.pad1 + t - QMAP_SEG < plan.end1) map[plan.pad1 + t - QMAP_SEG] = plan.v1;
+    for (int p = used + t; p < cap; p += QMAP_THREADS) map[p] = QMAP_EMPTY;
+}
+
 __global__ void wbc_reset_kernel(double* hist, const uint8_t* mask, int batch) {
     const int rb = xcd_robot();
     if (rb >= batch) return;
@@ -4345,7 +4440,11 @@ extern "C" hipError_t wbc_launch_step(const wbc::KernelArgs* a, hipStream_t st) 
     hipLaunchKernelGGL(wbc::wbc_step_kernel, dim3(a->batch), dim3(64), 0, st, *a);
     return hipGetLastError();
 }
-extern "C" int wbc_kernel_stance_elim() { return 1; }
+extern "C" hipError_t wbc_launch_qmap(const uint8_t* masks, int batch, int32_t* map, hipStream_t st) {
+    hipLaunchKernelGGL(wbc::wbc_qmap_kernel, dim3(1), dim3(wbc::QMAP_THREADS), 0, st, masks, batch, map,
+                       wbc::qmap_capacity(batch));
+    return hipGetLastError();
+}
 extern "C" hipError_t wbc_launch_update(const wbc::KernelArgs* a, hipStream_t st) {
     hipLaunchKernelGGL(wbc::wbc_update_kernel, dim3((a->batch + wbc::UPD_RPW - 1) / wbc::UPD_RPW), dim3(64), 0, st, *a);
     return hipGetLastError();
@@ -4365,8 +4464,9 @@ extern "C" hipError_t wbc_launch_solve_stance(const wbc::KernelArgs* a, hipStrea
 // QPs whose reduction was not usable with the general method in the same wave (drain_fallbacks:
 // their records carry their own mask and bounds, so the general solve runs them with modes = 0).
 extern "C" hipError_t wbc_launch_update_solve(const wbc::KernelArgs* a, hipStream_t st) {
-    hipLaunchKernelGGL(wbc::wbc_update_solve_kernel, dim3((a->batch + wbc::UPD_RPW - 1) / wbc::UPD_RPW), dim3(64), 0,
-                       st, *a);
+    static_assert(wbc::UPD_RPW == wbc::QMAP_SEG, "the wave map's segments are the kernel's");
+    if (a->nwaves <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(wbc::wbc_update_solve_kernel, dim3(a->nwaves), dim3(64), 0, st, *a);
     return hipGetLastError();
 }
 extern "C" hipError_t wbc_launch_reset(double* hist, const uint8_t* mask, int batch, hipStream_t st) {

@@ -152,12 +152,116 @@ struct KernelArgs {
     int32_t parity;
     int32_t* fb;
     int32_t fb_cap;
+    // The default step's wave map (wbc_update_solve_kernel): entry e = qmap[4 w + seg] of segment
+    // seg of workgroup w is (qp << 4 | mask) for a QP it solves (e >= 0), ~(qp << 4 | mask) for a
+    // padding segment that recomputes QP qp without writing anything, QMAP_EMPTY when the whole
+    // workgroup has nothing to do.  The mask travels in the entry, so the step reads one word before
+    // the QP's inputs (not the word and then contacts[qp]).  The engine groups the QPs by contact
+    // mask (qmap_build below, or wbc_qmap_kernel for device-bound masks), so the four segments of a
+    // wave share one mask.  nullptr: QP 4 w + seg (every mask in the step is equal).
+    // Under mode hypotheses the map is arithmetic (workgroup g K + k: states 4 g .. 4 g + 3 under
+    // mask modes[k]) and qmap is unused.  nwaves: the step kernel's grid.
+    const int32_t* qmap;
+    int32_t nwaves;
     // the parameters by value: read from the kernel-argument segment (scalar loads of memory the
     // compiler knows is constant), not through `params`, whose global loads it must repeat after
     // every global store and wait for in turn
     wbc_params pv;
 };
 
+// ---------------------------------------------------------------------------------------
+// Wave map of the default step: QPs grouped by contact mask, four to a wave (KernelArgs::qmap)
+// ---------------------------------------------------------------------------------------
+constexpr int32_t QMAP_EMPTY = (int32_t)0x80000000;
+constexpr int QMAP_MAX_BATCH = (1 << 27) - 1;  // qp << 4 fits 31 bits
+#ifdef __HIPCC__
+#define WBC_HD __host__ __device__
+#else
+#define WBC_HD
+#endif
+WBC_HD inline int32_t qmap_entry(int qp, int mask) { return (int32_t)((qp << 4) | (mask & 15)); }
+constexpr int QMAP_SEG = 4;  // QPs per wave (UPD_RPW of the kernel)
+// Layout.  The general 12-variable form runs one instruction stream for every contact mask, so
+// waves may mix masks at no cost; a stateless mask-15 QP takes the four-contact stance form, a
+// different stream, so it never shares a wave with another mask.  Within that rule the map groups
+// QPs of one mask (a wave runs its four QPs' largest pass count: QPs of one mask need similar counts)
+// and uses at most one wave more than ceil(B / 4), so a batch that fills whole rounds of the chip
+// does not spill a partial round:
+//   region 0: the r15 = cnt[15] % 4 mask-15 QPs left over from whole waves, padded to one wave
+//             (only when r15 > 0);
+//   region 1: the other masks' leftovers (< 4 each, at most 45) in mixed waves, the last padded;
+//   region 2: whole waves of one mask, buckets in QMAP_ORDER.
+// Leftovers are a bucket's last QPs in batch order; a bucket's other QPs keep their batch order;
+// padding segments recompute the bucket's first QP.  Buckets start with mask 15 (the most active-set
+// passes on the bench batches: 8.9 per QP against 6.7 for three stance legs and 0.3 for none), then
+// three stance legs, two, one, none: when a step has more waves than the chip holds at once, the
+// hardware starts them in map order, so the costliest start first and the cheapest fill the end.
+#ifndef WBC_QMAP_NATURAL_ORDER
+constexpr uint8_t QMAP_ORDER[16] = {15, 7, 11, 13, 14, 3, 5, 6, 9, 10, 12, 1, 2, 4, 8, 0};
+#else  // (A/B builds only)
+constexpr uint8_t QMAP_ORDER[16] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15};
+#endif
+// capacity of the map for B QPs (entries): ceil(B / 4) + 1 waves
+WBC_HD inline int qmap_capacity(int B) { return QMAP_SEG * ((B + QMAP_SEG - 1) / QMAP_SEG + 1); }
+struct QmapPlan {
+    int base1, base2, waves;  // region 1 / 2 starts (entries), total waves
+    int full[16];             // QPs of bucket m in whole waves (4 * floor(cnt / 4))
+    int off1[16], off2[16];   // bucket m's leftovers in region 1, its whole waves in region 2
+    int pad0, pad1, end1;     // padding: region 0 [pad0, 4), region 1 [pad1, end1)
+    int32_t v0, v1;           // their entries
+};
+// the plan from the bucket counts and each bucket's first QP (host and device builders alike)
+WBC_HD inline void qmap_plan(const int* cnt, const int* first, QmapPlan& p) {
+    const int r15 = cnt[15] % QMAP_SEG;
+    p.base1 = r15 ? QMAP_SEG : 0;
+    p.pad0 = r15;
+    p.v0 = ~qmap_entry(first[15] < 0 ? 0 : first[15], 15);
+    int o1 = 0, o2 = 0, last = -1;
+    for (int k = 0; k < 16; ++k) {
+        const int m = QMAP_ORDER[k];
+        p.full[m] = cnt[m] - cnt[m] % QMAP_SEG;
+        p.off2[m] = o2;
+        o2 += p.full[m];
+        p.off1[m] = o1;
+        if (m != 15 && cnt[m] % QMAP_SEG) {
+            o1 += cnt[m] % QMAP_SEG;
+            last = m;
+        }
+    }
+    p.pad1 = p.base1 + o1;
+    p.end1 = p.base1 + QMAP_SEG * ((o1 + QMAP_SEG - 1) / QMAP_SEG);
+    p.v1 = last < 0 ? 0 : ~qmap_entry(first[last], last);
+    p.base2 = p.end1;
+    p.waves = (p.base2 + o2) / QMAP_SEG;
+}
+// entry position of the j-th QP (batch order) of bucket m
+WBC_HD inline int qmap_pos(const QmapPlan& p, int m, int j) {
+    if (j < p.full[m]) return p.base2 + p.off2[m] + j;
+    const int i = j - p.full[m];
+    return (m == 15) ? i : p.base1 + p.off1[m] + i;
+}
+// Host form: returns the number of waves; 0 (map unused) when every mask is equal.
+inline int qmap_build(const uint8_t* masks, int B, int32_t* map) {
+    int cnt[16] = {0}, first[16];
+    for (int m = 0; m < 16; ++m) first[m] = -1;
+    for (int b = 0; b < B; ++b) {
+        const int m = masks[b] & 15;
+        if (first[m] < 0) first[m] = b;
+        ++cnt[m];
+    }
+    for (int m = 0; m < 16; ++m)
+        if (cnt[m] == B) return 0;
+    QmapPlan p;
+    qmap_plan(cnt, first, p);
+    int j[16] = {0};
+    for (int b = 0; b < B; ++b) {
+        const int m = masks[b] & 15;
+        map[qmap_pos(p, m, j[m]++)] = qmap_entry(b, m);
+    }
+    for (int e = p.pad0; p.base1 && e < QMAP_SEG; ++e) map[e] = p.v0;
+    for (int e = p.pad1; e < p.end1; ++e) map[e] = p.v1;
+    return p.waves;
+}
 
 
 }  // namespace wbc

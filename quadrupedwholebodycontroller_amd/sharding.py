@@ -127,3 +127,70 @@ def all_gather_rows(local, world: int, group=None):
     parts = [torch.empty_like(local) for _ in range(world)]
     dist.all_gather(parts, local.contiguous(), group=group)
     return torch.cat(parts)
+
+
+class StepPipeline:
+    """The per-step loop of bench.py on N ranks: every step writes the rank's outputs straight into a
+    packed block (StepOutputs, bound as the engine's output buffers) and the step's one collective
+    gathers the blocks on a second stream, overlapped with the next step.  Two blocks alternate: step
+    k + 2 waits for the gather of step k (an event on `comm`) before the engine overwrites its block.
+
+    engine: the rank's Engine (on `stream`); step(flags) runs one step (Engine.step or step_modes);
+    cap: rows of a block (the largest shard).  With world == 1 there is no gather (the block is the
+    whole batch's output).  tests/test_gpu_pipeline.py runs this class with two gloo ranks on one GPU
+    and checks every step's gathered outputs against a one-rank step."""
+
+    def __init__(self, engine, step, flags, world, cap, stream, comm=None, device="cuda", group=None):
+        import torch
+
+        self.torch = torch
+        self.e, self.step_fn, self.flags, self.world = engine, step, flags, world
+        self.stream, self.comm, self.group = stream, comm, group
+        self.cap = cap
+        self.blocks = [StepOutputs(cap, device=device) for _ in range(2)]
+        self.gathered = ([torch.empty(world * cap * ROW_DOUBLES, dtype=torch.float64, device=device)
+                          for _ in range(2)] if world > 1 else None)
+        self.ev_step = [torch.cuda.Event() for _ in range(2)]
+        self.ev_gath = [torch.cuda.Event() for _ in range(2)]
+        self.used = [False, False]
+        self.k = 0
+
+    def bind(self, slot):
+        b = self.blocks[slot]
+        self.e.bind_device_outputs(tau=b.tau.data_ptr(), status=b.status.data_ptr(), iters=b.iters.data_ptr())
+
+    def step(self):
+        """Queue one step (and, N > 1, its gather); returns the slot its outputs land in."""
+        torch = self.torch
+        slot = self.k & 1
+        if self.world > 1 and self.used[slot]:
+            self.stream.wait_event(self.ev_gath[slot])  # the gather of step k - 2 has read this block
+        self.bind(slot)
+        self.step_fn(self.flags)
+        if self.world > 1:
+            self.ev_step[slot].record(self.stream)
+            with torch.cuda.stream(self.comm):
+                self.comm.wait_event(self.ev_step[slot])
+                gather_step_outputs(self.blocks[slot], self.world, out=self.gathered[slot], group=self.group)
+                self.ev_gath[slot].record(self.comm)
+            self.used[slot] = True
+        self.k += 1
+        return slot
+
+    @property
+    def last_slot(self):
+        return (self.k - 1) & 1
+
+    def result(self, slot, total, unit=1):
+        """(tau, status, iters) of the step in `slot` for the whole batch (numpy, global order) once its
+        gather is done; `total` QPs overall (N > 1) or this rank's (N = 1)."""
+        import numpy as np
+
+        if self.world > 1:
+            self.ev_gath[slot].synchronize()
+            return unpack_gathered(self.gathered[slot], total, self.world, unit=unit)
+        self.ev_step[slot].record(self.stream)
+        self.ev_step[slot].synchronize()
+        b = self.blocks[slot]
+        return (b.tau[: total * TAU_W].cpu().numpy().reshape(total, TAU_W),
+                b.status[:total].cpu().numpy().astype(np.int32), b.iters[:total].cpu().numpy().astype(np.int32))

@@ -85,3 +85,26 @@ def test_cycle_keeps_bound_inputs():
     for k in KEYS:
         assert np.array_equal(got_b[k], want_b[k]), k
         assert np.array_equal(got_a[k], want_a[k]), k
+
+
+def test_cycle_graph_replay_across_flag_and_mask_changes():
+    """wbc_cycle replays a captured graph while its flags, stream and masks allow (every mask equal);
+    flag changes re-capture it and mixed masks take the eager path with the wave map.  Every cycle must
+    equal the separate calls, stateful history included."""
+    B = 8
+    seq = list(workloads.trot_sequence(B, steps=24, seed=9))
+    e1, e2 = Engine(B), Engine(B)
+    g = np.random.default_rng(2)
+    for t, s in enumerate(seq):
+        s = dict(s)
+        if t % 6 == 5:  # mixed masks: the eager path (wave map upload)
+            s["contacts"] = g.integers(0, 16, B).astype(np.uint8)
+        flags = 0  # stateful throughout; x on / off alternates below (a re-capture each change)
+        want = separate_calls(e1, s, flags)
+        got = e2.cycle(s["base_pose"], s["nu"], s["qj"], s["ref"], s["contacts"], s["switching"], flags,
+                       want_x=(t % 3 != 0))
+        for k in ("tau", "grf", "status", "iters"):
+            assert np.array_equal(got[k], want[k]), (t, k)
+        if t % 3 != 0:
+            assert np.array_equal(got["x"], want["x"]), t
+    e1.close(); e2.close()

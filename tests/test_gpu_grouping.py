@@ -1,0 +1,142 @@
+"""GPU: the default step groups its QPs by contact mask (KernelArgs::qmap), so a
+robot's outputs depend only on its own inputs, mask and flags, never on which robots share its wave.
+
+* A randomly permuted batch gives bit-identical per-robot outputs (tau, grf, x, status, iters) to the
+  unpermuted one: stateless rl_random with stretched legs (the in-wave fallback solve), and a
+  stateful run of mixed masks with hotstarts across 4 cycles (each engine's history evolves on its
+  own).
+* A robot solved inside a sub-batch (a shard, as on N ranks) equals the same robot in the full batch.
+* Device-bound masks equal host-copied masks, with the map built on the stream (WBC_GROUP,
+  wbc_qmap_kernel) and without one (waves of four consecutive, mixed-mask QPs: each segment takes
+  its own form), also on a permuted batch.
+* Mask-15 robots in a mixed stateless batch take the four-contact stance form, as in an all-stance
+  batch: bit-identical to the same robots stepped alone.
+* The grouped step still matches the C oracle (status equal, tau to 1e-7) on every mask.
+
+The reference solves one robot per call (cpp:650-652), so any dependence on batch neighbours would
+be an artefact of batching."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from quadrupedwholebodycontroller_amd import GROUP, NO_X, STATELESS, Engine, workloads  # noqa: E402
+
+KEYS = ("tau", "grf", "x", "status", "iters")
+
+
+def take(inp, idx):
+    return {k: np.ascontiguousarray(v[idx]) for k, v in inp.items()}
+
+
+def run(inp, flags=STATELESS, steps=1, engine=None):
+    B = len(inp["contacts"])
+    e = engine or Engine(B)
+    for _ in range(steps):
+        e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
+        e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
+        e.step(flags)
+    o = e.outputs()
+    if engine is None:
+        e.close()
+    return o
+
+
+def assert_rows_equal(a, b, idx_a=None, idx_b=None, what=""):
+    for k in KEYS:
+        va = a[k] if idx_a is None else a[k][idx_a]
+        vb = b[k] if idx_b is None else b[k][idx_b]
+        assert np.array_equal(va, vb), f"{what}: {k} differs on {int(np.sum(np.any((va != vb).reshape(len(va), -1), 1)))} robots"
+
+
+def test_permuted_batch_bit_identical():
+    inp = workloads.straight_legs(workloads.rl_random(1501, seed=21), every=7)
+    perm = np.random.default_rng(5).permutation(1501)
+    a = run(inp)
+    b = run(take(inp, perm))
+    assert_rows_equal(a, b, idx_a=perm, what="permuted stateless")
+    assert (a["status"] == 0).mean() > 0.5
+
+
+def test_subbatch_bit_identical():
+    inp = workloads.rl_random(1024, seed=22)
+    full = run(inp)
+    for lo, hi in ((0, 333), (333, 701), (701, 1024), (5, 6)):
+        part = run(take(inp, slice(lo, hi)))
+        assert_rows_equal(full, part, idx_a=slice(lo, hi), what=f"shard {lo}:{hi}")
+
+
+def test_stance_robots_in_mixed_batch_equal_all_stance_batch():
+    """Mask-15 robots of a mixed stateless batch take the stance form (one mask per wave)."""
+    st = workloads.stance_cold(257, seed=23)
+    rl = workloads.rl_random(400, seed=24)
+    mixed = {k: np.concatenate([st[k], rl[k]]) for k in st}
+    a = run(mixed)
+    b = run(st)
+    assert_rows_equal(a, b, idx_a=slice(0, 257), what="stance robots inside a mixed batch")
+
+
+def test_stateful_permuted_bit_identical():
+    B, steps = 777, 4
+    g = np.random.default_rng(25)
+    base = workloads.rl_random(B, seed=26)
+    base["switching"][:] = 0
+    perm = g.permutation(B)
+    ea, eb = Engine(B), Engine(B)
+    try:
+        for k in range(steps):
+            inp = {kk: v.copy() for kk, v in base.items()}
+            inp["qj"] = inp["qj"] + 0.002 * k
+            inp["contacts"] = g.integers(0, 16, B).astype(np.uint8) if k % 2 else base["contacts"]
+            a = run(inp, flags=0, engine=ea)
+            b = run(take(inp, perm), flags=0, engine=eb)
+            assert_rows_equal(a, b, idx_a=perm, what=f"stateful step {k}")
+    finally:
+        ea.close()
+        eb.close()
+
+
+@pytest.mark.parametrize("group", [True, False])
+def test_device_bound_masks_equal_host_masks(group):
+    B = 2050
+    inp = workloads.straight_legs(workloads.rl_random(B, seed=27), every=9)
+    a = run(inp, flags=STATELESS | NO_X)
+    flags = STATELESS | NO_X | (GROUP if group else 0)
+    perm = np.random.default_rng(3).permutation(B)
+    for order in (np.arange(B), perm):
+        src = take(inp, order)
+        e = Engine(B)
+        e.set_state(src["base_pose"], src["nu"], src["qj"])
+        e.set_reference(src["ref"], None, src["switching"])
+        dc = torch.from_numpy(src["contacts"]).to("cuda:0")
+        torch.cuda.synchronize()
+        e.bind_device_inputs(contacts=dc.data_ptr())
+        e.step(flags)
+        b = e.outputs()
+        # a mask change on the device: a map is rebuilt on the stream before every step
+        dc.copy_(torch.from_numpy(np.full(B, 15, np.uint8)))
+        torch.cuda.synchronize()
+        e.step(flags)
+        c = e.outputs()
+        e.close()
+        for k in ("tau", "grf", "status", "iters"):
+            assert np.array_equal(a[k][order], b[k]), (k, group)
+        st = dict(src, contacts=np.full(B, 15, np.uint8))
+        d = run(st, flags=STATELESS | NO_X)
+        for k in ("tau", "grf", "status", "iters"):
+            assert np.array_equal(c[k], d[k]), (k, group)
+
+
+def test_grouped_step_matches_oracle():
+    import wbc_ref
+
+    inp = workloads.rl_random(640, seed=28)
+    o = wbc_ref.run_batch(inp)
+    a = run(inp)
+    assert np.array_equal(a["status"], o["status"])
+    ok = a["status"] == 0
+    err = np.max(np.abs(a["tau"][ok] - o["tau"][ok]))
+    print(f"grouped rl_random B=640: max |tau - oracle| = {err:.3e} N m")
+    assert err < 1e-7

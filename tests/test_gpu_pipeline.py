@@ -1,0 +1,98 @@
+"""GPU: the multi-rank step loop of bench.py itself (sharding.StepPipeline), rehearsed with two gloo
+ranks sharing cuda:0 before the driver's first 8-GPU run executes it over RCCL.
+
+Each rank owns a contiguous shard of a global batch (strong scaling, as bench.py's rl_random_b65536 /
+modes16_x8192 configs; mode hypotheses shard by state), stages the inputs of every step in HBM and
+binds them per step (no host copy between steps, so the gather of step k, queued on the second
+stream, really overlaps step k + 1, and step k + 2 waits for it before reusing the block).  For each
+of 8 steps with changing inputs, the gathered tau | status | iters of the whole batch must equal a
+one-rank step of the full batch on the same inputs, bit for bit: the step groups QPs by contact mask,
+so a robot's result does not depend on where the shard boundary falls."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+WORKER = r"""
+import os, sys
+import numpy as np
+import torch, torch.distributed as dist
+sys.path.insert(0, {root!r})
+from quadrupedwholebodycontroller_amd import NO_X, STATELESS, Engine, workloads
+from quadrupedwholebodycontroller_amd.sharding import StepPipeline, shard_bounds, shard_capacity
+dist.init_process_group("gloo")
+rank, world = dist.get_rank(), dist.get_world_size()
+torch.cuda.set_device(0)
+STEPS = 8
+FLAGS = STATELESS | NO_X
+KEYS = ("base_pose", "nu", "qj", "ref", "contacts", "switching")
+
+def step_inputs(inp, k):
+    s = {{kk: v.copy() for kk, v in inp.items()}}
+    s["qj"] = s["qj"] + 0.003 * np.sin(k + np.arange(s["qj"].size).reshape(s["qj"].shape))
+    s["nu"] = s["nu"] * (1.0 + 0.05 * k)
+    return s
+
+def run(name, inp_all, modes):
+    K = len(modes) if modes is not None else 0
+    S = inp_all["base_pose"].shape[0]
+    total = S * (K or 1)
+    lo, hi = shard_bounds(S, world, rank)
+    cap = shard_capacity(S, world) * (K or 1)
+    seq = [step_inputs(inp_all, k) for k in range(STEPS)]
+    stream, comm = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    # this rank's shard of every step's inputs, staged in HBM
+    dev = {{kk: torch.from_numpy(np.ascontiguousarray(np.stack([s[kk][lo:hi] for s in seq]))).cuda() for kk in KEYS}}
+    e = Engine((hi - lo) * (K or 1))
+    e.set_stream(stream)
+    if K:
+        e.set_modes(modes)
+    step = e.step_modes if K else e.step
+    pipe = StepPipeline(e, step, FLAGS, world, cap, stream, comm)
+    results = []
+    for k in range(STEPS):
+        e.bind_device_inputs(*[dev[kk][k].data_ptr() for kk in KEYS])
+        slot = pipe.step()
+        if k >= 1:  # the previous step's gather, read while this step runs
+            results.append(pipe.result(1 - slot, total, unit=K or 1))
+    results.append(pipe.result(pipe.last_slot, total, unit=K or 1))
+    torch.cuda.synchronize()
+    e.close()
+    if rank == 0:  # the one-rank reference: the full batch, step by step
+        ref = Engine(total)
+        if K:
+            ref.set_modes(modes)
+        for k, s in enumerate(seq):
+            ref.set_state(s["base_pose"], s["nu"], s["qj"])
+            ref.set_reference(s["ref"], s["contacts"], s["switching"])
+            (ref.step_modes if K else ref.step)(FLAGS)
+            o = ref.outputs()
+            tau, st, it = results[k]
+            assert np.array_equal(tau, o["tau"]), (name, k, "tau")
+            assert np.array_equal(st, o["status"]) and np.array_equal(it, o["iters"]), (name, k)
+        ref.close()
+        print("CHECKED", name, total, flush=True)
+
+run("rl_random", workloads.rl_random(1337, seed=31), None)
+states, modes = workloads.mode_states(129, 32)
+run("modes16", states, modes)
+print("PIPE_OK", rank, flush=True)
+dist.destroy_process_group()
+"""
+
+
+def test_two_rank_step_pipeline_equals_one_rank(tmp_path):
+    script = tmp_path / "worker.py"
+    script.write_text(WORKER.format(root=ROOT))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=29541", str(script)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, (r.stdout[-1000:], r.stderr[-3000:])
+    assert "PIPE_OK 0" in r.stdout and "PIPE_OK 1" in r.stdout
+    assert "CHECKED rl_random" in r.stdout and "CHECKED modes16" in r.stdout

@@ -42,9 +42,11 @@ def test_caller_stream_matches_own_stream_and_switches_safely():
         out = e.outputs()
         for key in KEYS:
             assert np.array_equal(out[key], ref[k % 2][key]), (k, key)
-    e.set_stream(s.cuda_stream)
+    e.set_stream(s)  # the stream object: the engine keeps it referenced while bound
+    assert e._stream is s
     _load(e, a)
     for _ in range(5):
         e.step(STATELESS | NO_X)
-    e.close()  # drains the bound caller stream before freeing
+    e.close()  # drains the bound caller stream before freeing, then releases it
+    assert e._stream is None
     s.synchronize()
