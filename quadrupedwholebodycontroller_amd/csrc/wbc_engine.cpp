@@ -96,17 +96,22 @@ struct wbc_engine {
     // 0 = every mask equal, no map needed); for device-bound masks wbc_qmap_kernel builds it on the
     // stream before each step
     int32_t* d_qmap = nullptr;
+    const int32_t* qmap_dev = nullptr;  // the step's map of the engine's own masks: d_qmap, or m_qmap (zero-copy cycle)
+    const uint8_t* m_contacts = nullptr;  // the zero-copy cycle block's masks (device address)
+    // a zero-copy cycle ran last: the engine's own input / output blocks (and wave map) are behind the
+    // pinned ones until sync_own copies them (before any other call that reads or writes them)
+    bool zc_stale = false;
     int32_t* h_qmap = nullptr;  // pinned
     int32_t qmap_waves = 0;
     bool qmap_host = true;  // qmap_waves / d_qmap describe d_contacts (not after a change of modes)
     bool updated = false;
     bool timed = false;    // a WBC_TIMED step has recorded ev0 / ev1
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    // wbc_cycle's captured graph (H2D, step, D2H) and what it was captured for
-    hipGraphExec_t cyc_exec = nullptr;
-    uint32_t cyc_flags = 0;
-    hipStream_t cyc_stream = nullptr;
-    bool graph_ok = true;
+    // device addresses of the pinned cycle buffers (zero-copy cycle: the step reads h_in and writes
+    // h_out directly, no copies); null when the batch takes the copy path
+    const void* m_in = nullptr;
+    void* m_out = nullptr;
+    const int32_t* m_qmap = nullptr;
 };
 
 namespace {
@@ -122,6 +127,9 @@ size_t in_block_bytes(size_t B) {
 size_t out_block_bytes(size_t B) {
     return B * 2 * WBC_NUM_JOINTS * sizeof(double) + 2 * B * sizeof(int32_t) + B * WBC_NV * sizeof(double);
 }
+
+// wbc_cycle runs zero-copy up to this batch size (enqueue_cycle)
+[[maybe_unused]] constexpr size_t kZeroCopyMaxBatch = 64;
 
 // rows of the input arrays: one per robot, or one per state when mode hypotheses are set
 size_t input_rows(const wbc_engine* h) { return (size_t)(h->n_modes ? h->batch / h->n_modes : h->batch); }
@@ -200,6 +208,24 @@ int64_t count_stance(const uint8_t* masks, size_t n) {
     return c;
 }
 
+// After a zero-copy wbc_cycle the cycle's inputs, outputs and wave map live in the pinned blocks;
+// copy them into the engine's own device buffers, so every other call sees the state a copying
+// cycle leaves (synchronous: the pinned blocks are rewritten by the next cycle).
+hipError_t sync_own(wbc_engine* h) {
+    if (!h->zc_stale) return hipSuccess;
+    const size_t B = (size_t)h->batch;
+    hipError_t e = hipSetDevice(h->device);
+    if (e == hipSuccess) e = hipMemcpyAsync(h->d_inblk, h->h_in, in_block_bytes(B), hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(h->d_outblk, h->h_out, out_block_bytes(B), hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess && h->qmap_waves)
+        e = hipMemcpyAsync(h->d_qmap, h->h_qmap, (size_t)h->qmap_waves * wbc::QMAP_SEG * sizeof(int32_t),
+                           hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e == hipSuccess) h->zc_stale = false;
+    return e;
+}
+
 // Stance elimination for this update: on when every QP has mask 15 (a mixed batch would pay the
 // elimination in the update kernel's mixed waves and a second solve kernel's latency; measured
 // slower, profiles/r02/k), which the host knows for its own contact masks and for mode masks.
@@ -231,10 +257,10 @@ hipError_t begin_step16(wbc_engine* h, wbc::KernelArgs& a, uint32_t flags) {
         a.nwaves = ((S + wbc::QMAP_SEG - 1) / wbc::QMAP_SEG) * a.modes;
         return hipSuccess;
     }
-    if (h->in_contacts == h->d_contacts && h->qmap_host) {
+    if ((h->in_contacts == h->d_contacts || (h->m_contacts && h->in_contacts == h->m_contacts)) && h->qmap_host) {
 #ifndef WBC_NO_QMAP  // (A/B builds only: the unmapped step)
         if (h->qmap_waves) {
-            a.qmap = h->d_qmap;
+            a.qmap = h->qmap_dev;
             a.nwaves = h->qmap_waves;
         }
 #endif
@@ -340,10 +366,11 @@ int32_t wbc_create(const wbc_model* model, const wbc_params* params, int32_t bat
     ALLOC(d_dbg, B * WBC_DBG_LEN);
     ALLOC(d_qmap, wbc::qmap_capacity(batch));
 #undef ALLOC
-    if (hipHostMalloc(&h->h_qmap, sizeof(int32_t) * wbc::qmap_capacity(batch), hipHostMallocDefault) != hipSuccess) {
+    if (hipHostMalloc(&h->h_qmap, sizeof(int32_t) * wbc::qmap_capacity(batch), hipHostMallocMapped) != hipSuccess) {
         wbc_destroy(h);
         return fail(WBC_ERR_HIP, "hipHostMalloc failed: wave map");
     }
+    h->qmap_dev = h->d_qmap;
     if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) {
         wbc_destroy(h);
@@ -402,7 +429,6 @@ int32_t wbc_destroy(wbc_engine* h) {
     if (h->h_in) (void)hipHostFree(h->h_in);
     if (h->h_out) (void)hipHostFree(h->h_out);
     if (h->h_qmap) (void)hipHostFree(h->h_qmap);
-    if (h->cyc_exec) (void)hipGraphExecDestroy(h->cyc_exec);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
@@ -427,6 +453,7 @@ int32_t wbc_set_stream(wbc_engine* h, void* stream) {
 
 int32_t wbc_set_state(wbc_engine* h, const double* base_pose, const double* nu, const double* qj) {
     if (!h) return fail(WBC_ERR_ARG, "null handle");
+    WBC_HIP(sync_own(h));
     WBC_HIP(hipSetDevice(h->device));
     const size_t B = input_rows(h);
     if (base_pose) { WBC_HIP(hipMemcpyAsync(h->d_pose, base_pose, B * WBC_POSE_LEN * sizeof(double), hipMemcpyHostToDevice, h->stream)); h->in_pose = h->d_pose; }
@@ -438,6 +465,7 @@ int32_t wbc_set_state(wbc_engine* h, const double* base_pose, const double* nu, 
 
 int32_t wbc_set_reference(wbc_engine* h, const double* ref, const uint8_t* contacts, const uint8_t* switching) {
     if (!h) return fail(WBC_ERR_ARG, "null handle");
+    WBC_HIP(sync_own(h));
     WBC_HIP(hipSetDevice(h->device));
     const size_t B = input_rows(h);
     if (ref) { WBC_HIP(hipMemcpyAsync(h->d_ref, ref, B * WBC_REF_LEN * sizeof(double), hipMemcpyHostToDevice, h->stream)); h->in_ref = h->d_ref; }
@@ -478,6 +506,7 @@ int32_t wbc_bind_device_outputs(wbc_engine* h, double* d_tau, double* d_grf, dou
 
 int32_t wbc_reset(wbc_engine* h, const uint8_t* mask) {
     if (!h) return fail(WBC_ERR_ARG, "null handle");
+    WBC_HIP(sync_own(h));
     WBC_HIP(hipSetDevice(h->device));
     const uint8_t* dm = nullptr;
     if (mask) {
@@ -492,6 +521,7 @@ int32_t wbc_reset(wbc_engine* h, const uint8_t* mask) {
 
 int32_t wbc_update(wbc_engine* h, uint32_t flags) {
     if (!h) return fail(WBC_ERR_ARG, "null handle");
+    WBC_HIP(sync_own(h));
     if (h->n_modes) return fail(WBC_ERR_STATE, "wbc_update: mode hypotheses are set (use wbc_step_modes, or wbc_set_modes(h, 0, NULL))");
     WBC_HIP(hipSetDevice(h->device));
     wbc::KernelArgs a = make_args(h, flags);
@@ -503,6 +533,7 @@ int32_t wbc_update(wbc_engine* h, uint32_t flags) {
 
 int32_t wbc_solve(wbc_engine* h, uint32_t flags) {
     if (!h) return fail(WBC_ERR_ARG, "null handle");
+    WBC_HIP(sync_own(h));
     if (h->n_modes) return fail(WBC_ERR_STATE, "wbc_solve: mode hypotheses are set (use wbc_step_modes, or wbc_set_modes(h, 0, NULL))");
     if (!h->updated) return fail(WBC_ERR_STATE, "wbc_solve before wbc_update");
     WBC_HIP(hipSetDevice(h->device));
@@ -513,6 +544,7 @@ int32_t wbc_solve(wbc_engine* h, uint32_t flags) {
 
 int32_t wbc_step(wbc_engine* h, uint32_t flags) {
     if (!h) return fail(WBC_ERR_ARG, "null handle");
+    WBC_HIP(sync_own(h));
     if (h->n_modes) return fail(WBC_ERR_STATE, "wbc_step: mode hypotheses are set (use wbc_step_modes, or wbc_set_modes(h, 0, NULL))");
     WBC_HIP(hipSetDevice(h->device));
     wbc::KernelArgs a = make_args(h, flags);
@@ -540,6 +572,7 @@ int32_t wbc_step(wbc_engine* h, uint32_t flags) {
 
 int32_t wbc_set_modes(wbc_engine* h, int32_t n_modes, const uint8_t* modes) {
     if (!h) return fail(WBC_ERR_ARG, "null handle");
+    WBC_HIP(sync_own(h));
     // contacts[] copied while modes were set hold S rows only: the engine's own masks get their
     // wave map on the device from here on, until the next wbc_set_reference / wbc_cycle with masks
     h->qmap_host = false;
@@ -561,6 +594,7 @@ int32_t wbc_set_modes(wbc_engine* h, int32_t n_modes, const uint8_t* modes) {
 
 int32_t wbc_step_modes(wbc_engine* h, uint32_t flags) {
     if (!h) return fail(WBC_ERR_ARG, "null handle");
+    WBC_HIP(sync_own(h));
     if (!h->n_modes) return fail(WBC_ERR_STATE, "wbc_step_modes: no mode hypotheses set (wbc_set_modes)");
     if (!(flags & WBC_STATELESS)) return fail(WBC_ERR_ARG, "wbc_step_modes: hypotheses are cold steps (WBC_STATELESS)");
     if (flags & WBC_DEBUG) return fail(WBC_ERR_ARG, "wbc_step_modes: no debug records for hypotheses");
@@ -597,29 +631,46 @@ namespace {
 // engine's own input and output buffers (caller bindings are restored afterwards), one D2H copy
 // (x, last in the block, only without WBC_NO_X).
 int32_t enqueue_cycle(wbc_engine* h, uint32_t flags) {
+    h->zc_stale = false;  // this cycle's blocks replace whatever was pending
     const size_t B = (size_t)h->batch;
     const size_t inb = in_block_bytes(B), outb = out_block_bytes(B), xb = B * WBC_NV * sizeof(double);
-    WBC_HIP(hipMemcpyAsync(h->d_inblk, h->h_in, inb, hipMemcpyHostToDevice, h->stream));
-    if (h->qmap_waves)
-        WBC_HIP(hipMemcpyAsync(h->d_qmap, h->h_qmap, (size_t)h->qmap_waves * wbc::QMAP_SEG * sizeof(int32_t),
-                               hipMemcpyHostToDevice, h->stream));
+    const bool zc = h->m_in != nullptr;
+    if (!zc) {
+        WBC_HIP(hipMemcpyAsync(h->d_inblk, h->h_in, inb, hipMemcpyHostToDevice, h->stream));
+        if (h->qmap_waves)
+            WBC_HIP(hipMemcpyAsync(h->d_qmap, h->h_qmap, (size_t)h->qmap_waves * wbc::QMAP_SEG * sizeof(int32_t),
+                                   hipMemcpyHostToDevice, h->stream));
+    }
+    // the step's input and output block: the engine's device buffers, or (zero-copy) the pinned
+    // host buffers through their device addresses, in the same layouts
+    const double* ib = zc ? static_cast<const double*>(h->m_in) : static_cast<const double*>(h->d_inblk);
+    double* ob = zc ? static_cast<double*>(h->m_out) : static_cast<double*>(h->d_outblk);
     const double* const ip = h->in_pose; const double* const in = h->in_nu; const double* const iq = h->in_qj;
     const double* const ir = h->in_ref; const uint8_t* const ic = h->in_contacts; const uint8_t* const is = h->in_switching;
-    h->in_pose = h->d_pose;
-    h->in_nu = h->d_nu;
-    h->in_qj = h->d_qj;
-    h->in_ref = h->d_ref;
-    h->in_contacts = h->d_contacts;
-    h->in_switching = h->d_switching;
+    h->in_pose = ib;
+    h->in_nu = ib + B * WBC_POSE_LEN;
+    h->in_qj = h->in_nu + B * WBC_NU_LEN;
+    h->in_ref = h->in_qj + B * WBC_NUM_JOINTS;
+    h->in_contacts = reinterpret_cast<const uint8_t*>(h->in_ref + B * WBC_REF_LEN);
+    h->in_switching = h->in_contacts + B;
     double* const bt = h->out_tau; double* const bg = h->out_grf; double* const bx = h->out_x;
     int32_t* const bs = h->out_status; int32_t* const bi = h->out_iters;
-    h->out_tau = h->d_tau; h->out_grf = h->d_grf; h->out_x = h->d_x; h->out_status = h->d_status; h->out_iters = h->d_iters;
+    h->out_tau = ob;
+    h->out_grf = ob + B * WBC_NUM_JOINTS;
+    h->out_status = reinterpret_cast<int32_t*>(h->out_grf + B * WBC_NUM_JOINTS);
+    h->out_iters = h->out_status + B;
+    h->out_x = reinterpret_cast<double*>(h->out_iters + B);
+    const int32_t* const qm = h->qmap_dev;
+    if (zc) h->qmap_dev = h->m_qmap;
     const int32_t rc = wbc_step(h, flags);
+    h->qmap_dev = qm;
     h->out_tau = bt; h->out_grf = bg; h->out_x = bx; h->out_status = bs; h->out_iters = bi;
     h->in_pose = ip; h->in_nu = in; h->in_qj = iq; h->in_ref = ir; h->in_contacts = ic; h->in_switching = is;
     if (rc != WBC_OK) return rc;
-    WBC_HIP(hipMemcpyAsync(h->h_out, h->d_outblk, (flags & WBC_NO_X) ? outb - xb : outb, hipMemcpyDeviceToHost,
-                           h->stream));
+    h->zc_stale = zc;
+    if (!zc)
+        WBC_HIP(hipMemcpyAsync(h->h_out, h->d_outblk, (flags & WBC_NO_X) ? outb - xb : outb, hipMemcpyDeviceToHost,
+                               h->stream));
     return WBC_OK;
 }
 }  // namespace
@@ -635,8 +686,26 @@ int32_t wbc_cycle(wbc_engine* h, const double* base_pose, const double* nu, cons
     const size_t B = (size_t)h->batch;
     const size_t inb = in_block_bytes(B), outb = out_block_bytes(B);
     if (!h->h_in) {
-        WBC_HIP(hipHostMalloc(&h->h_in, inb, hipHostMallocDefault));
-        WBC_HIP(hipHostMalloc(&h->h_out, outb, hipHostMallocDefault));
+        WBC_HIP(hipHostMalloc(&h->h_in, inb, hipHostMallocMapped));
+        WBC_HIP(hipHostMalloc(&h->h_out, outb, hipHostMallocMapped));
+#ifndef WBC_CYCLE_COPY  // (A/B builds only: the copy cycle at every batch size)
+        // Small batches (the B = 1 drop-in) run zero-copy: the step reads the pinned input block and
+        // writes the pinned output block through their device addresses (a few hundred bytes over
+        // PCIe inside the kernel instead of an H2D and a D2H copy, each a separate queued operation).
+        if (B <= kZeroCopyMaxBatch) {
+            void *mi = nullptr, *mo = nullptr, *mq = nullptr;
+            if (hipHostGetDevicePointer(&mi, h->h_in, 0) == hipSuccess &&
+                hipHostGetDevicePointer(&mo, h->h_out, 0) == hipSuccess &&
+                hipHostGetDevicePointer(&mq, h->h_qmap, 0) == hipSuccess) {
+                h->m_in = mi;
+                h->m_out = mo;
+                h->m_qmap = static_cast<const int32_t*>(mq);
+                h->m_contacts = reinterpret_cast<const uint8_t*>(static_cast<const double*>(mi) +
+                                                                 B * (WBC_POSE_LEN + WBC_NU_LEN + WBC_NUM_JOINTS + WBC_REF_LEN));
+            }
+            (void)hipGetLastError();
+        }
+#endif
     }
     // pack the host inputs in the device block's layout (pinned), one H2D copy
     double* hp = static_cast<double*>(h->h_in);
@@ -654,38 +723,7 @@ int32_t wbc_cycle(wbc_engine* h, const double* base_pose, const double* nu, cons
     h->qmap_waves = wbc::qmap_build(contacts, h->batch, h->h_qmap);  // uploaded by enqueue_cycle
     h->qmap_host = true;
     if (!x) flags |= WBC_NO_X;
-    // Replayed from a captured HIP graph (H2D copy, step kernel, D2H copy: one launch call instead
-    // of three) while nothing in it changes: the same flags and stream and no wave map to upload
-    // (every mask equal, e.g. the B = 1 drop-in), not split (its update alternates fallback counters)
-    // or timed.  Otherwise, and if capture fails, enqueued eagerly.
-#ifndef WBC_NO_CYCLE_GRAPH  // (A/B builds only: the eager cycle)
-    const bool graphable = h->qmap_waves == 0 && !(flags & (WBC_TIMED | WBC_SPLIT)) && h->graph_ok;
-#else
-    const bool graphable = false;
-#endif
-    if (graphable && h->cyc_exec && (h->cyc_flags != flags || h->cyc_stream != h->stream)) {
-        (void)hipGraphExecDestroy(h->cyc_exec);
-        h->cyc_exec = nullptr;
-    }
-    if (graphable && !h->cyc_exec) {
-        hipGraph_t g = nullptr;
-        bool ok = hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal) == hipSuccess;
-        const int32_t rc = ok ? enqueue_cycle(h, flags) : WBC_OK;
-        ok = (hipStreamEndCapture(h->stream, &g) == hipSuccess) && ok && rc == WBC_OK && g;
-        ok = ok && hipGraphInstantiate(&h->cyc_exec, g, nullptr, nullptr, 0) == hipSuccess;
-        if (g) (void)hipGraphDestroy(g);
-        if (!ok) {  // e.g. a stream that cannot be captured: eager from now on
-            h->cyc_exec = nullptr;
-            h->graph_ok = false;
-            (void)hipGetLastError();
-        } else {
-            h->cyc_flags = flags;
-            h->cyc_stream = h->stream;
-        }
-    }
-    if (graphable && h->cyc_exec) {
-        WBC_HIP(hipGraphLaunch(h->cyc_exec, h->stream));
-    } else {
+    {
         const int32_t rc = enqueue_cycle(h, flags);
         if (rc != WBC_OK) return rc;
     }
@@ -710,6 +748,7 @@ int32_t wbc_synchronize(wbc_engine* h) {
 
 int32_t wbc_get_output(wbc_engine* h, double* tau, double* grf, double* x, int32_t* status, int32_t* iters) {
     if (!h) return fail(WBC_ERR_ARG, "null handle");
+    WBC_HIP(sync_own(h));
     WBC_HIP(hipSetDevice(h->device));
     const size_t B = (size_t)h->batch;
     hipStream_t st = h->stream;
@@ -725,6 +764,7 @@ int32_t wbc_get_output(wbc_engine* h, double* tau, double* grf, double* x, int32
 int32_t wbc_device_outputs(wbc_engine* h, double** d_tau, double** d_grf, double** d_x, int32_t** d_status,
                            int32_t** d_iters) {
     if (!h) return fail(WBC_ERR_ARG, "null handle");
+    WBC_HIP(sync_own(h));
     if (d_tau) *d_tau = h->out_tau;
     if (d_grf) *d_grf = h->out_grf;
     if (d_x) *d_x = h->out_x;

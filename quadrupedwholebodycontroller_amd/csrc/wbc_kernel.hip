@@ -821,9 +821,13 @@ __device__ bool stance_reduce([[maybe_unused]] const KernelArgs& ka, [[maybe_unu
     {
         const int ra = lane % 6, h = (lane / 6) & 1;
         double acc[4][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+        // both K entries loaded unconditionally and selected: a load under the lane-dependent
+        // condition became a branch with its own LDS wait, 12 serialized round trips
+        const int ra3 = ra < 3 ? ra : 0, rk3 = ra < 3 ? 0 : ra - 3;
 #pragma unroll
         for (int j = 0; j < 12; ++j) {
-            const double kj = (ra < 3) ? s.A[j][ra] * inv_m : s.KA[j][ra < 3 ? 0 : ra - 3];
+            const double av = s.A[j][ra3], kv = s.KA[j][rk3];
+            const double kj = (ra < 3) ? av * inv_m : kv;
 #pragma unroll
             for (int c = 0; c < 3; ++c) acc[c][j & 3] = fma(kj, R.W[j][3 * h + c], acc[c][j & 3]);
             acc[3][j & 3] = fma(kj, R.w[j], acc[3][j & 3]);
@@ -1357,9 +1361,13 @@ __device__ bool reduce_general([[maybe_unused]] const KernelArgs& ka, [[maybe_un
     {
         const int ra = lane % 6, h = (lane / 6) & 1;
         double acc[4][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+        // both K entries loaded unconditionally and selected: a load under the lane-dependent
+        // condition became a branch with its own LDS wait, 12 serialized round trips
+        const int ra3 = ra < 3 ? ra : 0, rk3 = ra < 3 ? 0 : ra - 3;
 #pragma unroll
         for (int j = 0; j < 12; ++j) {
-            const double kj = (ra < 3) ? s.A[j][ra] * inv_m : s.KA[j][ra < 3 ? 0 : ra - 3];
+            const double av = s.A[j][ra3], kv = s.KA[j][rk3];
+            const double kj = (ra < 3) ? av * inv_m : kv;
 #pragma unroll
             for (int c = 0; c < 3; ++c) acc[c][j & 3] = fma(kj, R.W[j][3 * h + c], acc[c][j & 3]);
             acc[3][j & 3] = fma(kj, R.w[j], acc[3][j & 3]);
@@ -1665,7 +1673,8 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
                         : (r == 1) ? ((rr == 2) ? -1.0 : (rr == 3 ? 1.0 : 0.0)) : pr.friction;
         n0[m] = (m / 3 == fl) ? fv : 0.0;
         n1[m] = -sg * V.Nt[k1 * NTS + m];
-        n2[m] = v2 ? -sg * V.Nt[k2 * NTS + m] : 0.0;
+        const double nt2 = V.Nt[k2 * NTS + m];  // (k2 is a valid row in every lane: loaded, then masked)
+        n2[m] = v2 ? -sg * nt2 : 0.0;
     }
     const double bp1 = -pr.max_torque - sg * V.t0[k1], bp2 = -pr.max_torque - sg * V.t0[k2];
     const double tol0 = 1e-10;
@@ -2433,11 +2442,16 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
         const double aj[3] = {s.ja[j][0], s.ja[j][1], s.ja[j][2]};
         const double oj[3] = {s.jo[j][0], s.jo[j][1], s.jo[j][2]};
         double Al[3] = {0, 0, 0}, Aa[3] = {0, 0, 0}, hsum[3] = {0, 0, 0}, Mrow[3] = {0, 0, 0};
+        // every lane runs the three bodies of its leg, the ones above its joint weighted by 0: a
+        // lane-dependent `if (kk >= k)` put each body's LDS loads in an exec-masked block with its
+        // own wait (SUB = 16; the 64-lane kernel keeps the branch, its registers are tighter)
 #pragma unroll
         for (int kk = 0; kk < 3; ++kk) {
-            if (kk >= k) {
+            const bool below = kk >= k;
+            if (SUB == 16 || below) {
                 const int b = 1 + 3 * l + kk;
-                const double mb = md.link[l][kk].mass;
+                const double mb = (SUB == 16 && !below) ? 0.0 : md.link[l][kk].mass;
+                const double wI = (SUB == 16 && !below) ? 0.0 : 1.0;  // the inertia and force terms
                 const Body& bd = s.bd[b];
                 const double cb[3] = {bd.c[0], bd.c[1], bd.c[2]};
                 double rel[3] = {cb[0] - oj[0], cb[1] - oj[1], cb[2] - oj[2]}, v[3], t[3], Ia[3], fm[3];
@@ -2447,10 +2461,12 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
                 mv3(bd.I, aj, Ia);
                 cross3(rel, bd.F, fm);
 #pragma unroll
+                for (int i = 0; i < 3; ++i) Ia[i] *= wI;
+#pragma unroll
                 for (int i = 0; i < 3; ++i) {
                     Al[i] += mb * v[i];
                     Aa[i] += mb * t[i] + Ia[i];
-                    hsum[i] += fm[i] + bd.N[i];
+                    hsum[i] += wI * (fm[i] + bd.N[i]);
                 }
 #pragma unroll
                 for (int k2 = 0; k2 < 3; ++k2) {
@@ -2573,8 +2589,8 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
     // dt (an IEEE division is ~10 dependent instructions; the two agree to an ulp)
     const double rdt = pr.loop_rate;
 
-    // lane = joint column j: Jbar joint column, Mbar_j column, bbar_j
-    if (lane < 12) {
+    if constexpr (SUB == 64) {  // the fused kernel (2 waves per SIMD): stores in the loops, no spills
+      if (lane < 12) {
         const int j = lane, lj = j / 3, kj = j % 3;
         const double Alj[3] = {s.A[j][0], s.A[j][1], s.A[j][2]}, Aaj[3] = {s.A[j][3], s.A[j][4], s.A[j][5]};
         const double KAj[3] = {s.KA[j][0], s.KA[j][1], s.KA[j][2]};
@@ -2600,6 +2616,44 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
         const double hpj = s.hj[j] + dot3(Alj, y) + (t[0] + Aaj[0]) * y[3] + (t[1] + Aaj[1]) * y[4] + (t[2] + Aaj[2]) * y[5];
         P.bbj[j] = hpj - (dot3(Alj, zeta) + dot3(Aaj, &zeta[3]));
         P.d[j] = s.pf[lj][kj] - sel3(c, kj);
+      }
+    } else
+    // lane = joint column j: Jbar joint column, Mbar_j column, bbar_j.  The lane's own values are
+    // loaded unconditionally and the stage's stores come after its loads: a load under a
+    // lane-dependent condition became an exec-masked block with its own LDS wait, and a store
+    // between loads kept the compiler from moving the later loads up (~50 LDS waits before)
+    if (lane < 12) {
+        const int j = lane, lj = j / 3, kj = j % 3;
+        const double Alj[3] = {s.A[j][0], s.A[j][1], s.A[j][2]}, Aaj[3] = {s.A[j][3], s.A[j][4], s.A[j][5]};
+        const double KAj[3] = {s.KA[j][0], s.KA[j][1], s.KA[j][2]};
+        const double mjr[3] = {s.Mjj[j][0], s.Mjj[j][1], s.Mjj[j][2]};
+        const double jfo[3] = {s.Jf[lj][kj], s.Jf[lj][3 + kj], s.Jf[lj][6 + kj]};  // own leg's column
+        double jb[12];
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+            double d[3] = {s.pf[l][0] - c[0], s.pf[l][1] - c[1], s.pf[l][2] - c[2]}, t[3];
+            cross3(d, KAj, t);
+#pragma unroll
+            for (int rr = 0; rr < 3; ++rr) jb[3 * l + rr] = ((l == lj) ? jfo[rr] : 0.0) - Alj[rr] * inv_m + t[rr];
+        }
+#pragma unroll
+        for (int i = 0; i < 12; ++i) P.Jbj[i * 12 + j] = jb[i];  // (before the M-bar loads: its live range ends)
+        double mcol[12];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+            double Mij = (i / 3 == lj) ? mjr[i % 3] : 0.0;
+            Mij -= (s.A[i][0] * Alj[0] + s.A[i][1] * Alj[1] + s.A[i][2] * Alj[2]) * inv_m;
+            Mij -= s.A[i][3] * KAj[0] + s.A[i][4] * KAj[1] + s.A[i][5] * KAj[2];
+            mcol[i] = Mij;
+        }
+        double t[3];
+        cross3(r, Alj, t);
+        const double hpj = s.hj[j] + dot3(Alj, y) + (t[0] + Aaj[0]) * y[3] + (t[1] + Aaj[1]) * y[4] + (t[2] + Aaj[2]) * y[5];
+        const double dj = s.pf[lj][kj] - sel3(c, kj);
+#pragma unroll
+        for (int i = 0; i < 12; ++i) P.Mbj[i * 12 + j] = mcol[i];
+        P.bbj[j] = hpj - (dot3(Alj, zeta) + dot3(Aaj, &zeta[3]));
+        P.d[j] = dj;
     }
     UST(a, rb, 8);
     // T_top = [Ad^-1(r), Mbar_b^-1 A_j]; Tdot_inv for the next cycle (cpp:291-293)
@@ -2617,20 +2671,25 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
 #pragma unroll
         for (int it = 0; it < NT; ++it) {
         const int ln = lane + it * SUB;
+        // this lane's joint column (clamped, so every lane loads: the loads are not left inside the
+        // lane-dependent branch below, where each waited for its own LDS round trip)
+        const int jc = ln < 6 ? 0 : (ln > 17 ? 11 : ln - 6);
+        double Aj[3], KAj[3];
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr) { Aj[rr] = s.A[jc][rr]; KAj[rr] = s.KA[jc][rr]; }
         if (ln >= 3 && ln < 6) {  // lin rows, cols 3..5: S(dr)
             const int cc = ln - 3;
             double e[3] = {cc == 0 ? 1.0 : 0.0, cc == 1 ? 1.0 : 0.0, cc == 2 ? 1.0 : 0.0};
             cross3(dr, e, tcol[it]);
         } else if (ln >= 6 && ln < 18) {
-            const int j = ln - 6;
             double Tj[6];
 #pragma unroll
             for (int rr = 0; rr < 3; ++rr) {
-                Tj[rr] = switching ? 0.0 : (s.A[j][rr] * inv_m - hMa[it][rr]) * rdt;
-                Tj[3 + rr] = switching ? 0.0 : (s.KA[j][rr] - hMa[it][3 + rr]) * rdt;
+                Tj[rr] = switching ? 0.0 : (Aj[rr] * inv_m - hMa[it][rr]) * rdt;
+                Tj[3 + rr] = switching ? 0.0 : (KAj[rr] - hMa[it][3 + rr]) * rdt;
             }
             double t1[3], t2[3];
-            cross3(dr, s.KA[j], t1);
+            cross3(dr, KAj, t1);
             cross3(r, &Tj[3], t2);
 #pragma unroll
             for (int rr = 0; rr < 3; ++rr) {

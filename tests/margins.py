@@ -1,0 +1,44 @@
+"""Parity margins: what each GPU parity test actually achieved against its bound.
+
+Tests call `record(quantity, achieved, bound)` (an error normalised as the test normalises it, or a
+mismatch fraction) and `close(a, b, tol, quantity)` for the usual max|a - b| <= tol (1 + max|b|)
+check.  Each record is printed (visible with pytest -s / -v on failure) and kept per (test,
+quantity) as the worst value seen; conftest.py writes them at the end of the session to
+$WBC_MARGINS_OUT (default gpurun_out/parity_margins.json) as
+{test: {quantity: {"achieved", "bound", "margin" = bound / achieved}}}."""
+import os
+
+import numpy as np
+
+_RECORDS = {}
+
+
+def _test_id():
+    return os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0]
+
+
+def record(quantity, achieved, bound):
+    achieved = float(achieved)
+    t = _RECORDS.setdefault(_test_id(), {})
+    cur = t.get(quantity)
+    if cur is None or achieved > cur["achieved"]:
+        t[quantity] = {"achieved": achieved, "bound": float(bound),
+                       "margin": (float(bound) / achieved) if achieved > 0 else None}
+    print(f"[margin] {_test_id()} {quantity}: {achieved:.3e} (bound {bound:.1e})")
+    return achieved
+
+
+def norm_err(a, b):
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    if a.size == 0:
+        return 0.0
+    return float(np.max(np.abs(a - b)) / (1.0 + np.max(np.abs(b))))
+
+
+def close(a, b, tol, quantity="max|a-b|/(1+max|b|)"):
+    """max|a - b| <= tol (1 + max|b|), with the achieved value recorded."""
+    return record(quantity, norm_err(a, b), tol) <= tol
+
+
+def records():
+    return _RECORDS

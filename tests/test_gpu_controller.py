@@ -13,6 +13,8 @@ import os
 import subprocess
 
 import numpy as np
+
+import margins as M
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -22,9 +24,8 @@ BIN = os.path.join(ROOT, "quadrupedwholebodycontroller_amd", "wbc_control_loop")
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
-def close_to(a, b, tol):
-    a, b = np.asarray(a), np.asarray(b)
-    return np.max(np.abs(a - b)) <= tol * (1 + np.max(np.abs(b)))
+def close_to(a, b, tol, quantity="value"):
+    return M.close(a, b, tol, quantity)
 
 
 @pytest.mark.parametrize("name", ["traj_stance_hold", "traj_trot"])
@@ -45,8 +46,8 @@ def test_controller_shim_replays_golden(name, tmp_path):
     assert np.array_equal(out[:, 0].astype(int), g["out_status"][:, 0])
     for t in range(T):
         if g["out_status"][t, 0] == 0:
-            assert close_to(out[t, 2:14], g["out_tau"][t, 0], 1e-7), t
-            assert close_to(out[t, 14:56], g["out_x"][t, 0], 1e-7), t
+            assert close_to(out[t, 2:14], g["out_tau"][t, 0], 1e-7, "tau"), t
+            assert close_to(out[t, 14:56], g["out_x"][t, 0], 1e-7, "x"), t
 
 
 def test_controller_stance_harness():
@@ -69,4 +70,4 @@ def test_controller_run_spins_callbacks_beside_the_control_thread():
     assert res["cycles"] == 300 and res["qp_status"] == 0 and res["messages"] > 0
     s = subprocess.run([BIN, "stance", "300"], capture_output=True, text=True, timeout=300)
     ref = json.loads(s.stdout.strip().splitlines()[-1])
-    assert close_to(res["tau"], ref["tau"], 1e-9), (res["tau"], ref["tau"])
+    assert close_to(res["tau"], ref["tau"], 1e-9, "tau"), (res["tau"], ref["tau"])

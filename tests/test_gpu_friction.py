@@ -5,6 +5,8 @@ cpp:122-148; the pyramid rows at cpp:404-424) the engine matches the C oracle's 
 on every robot, status included, on the four-contact stance batch (the friction faces bind more
 often at small mu) and on random states over all 16 contact masks."""
 import numpy as np
+
+import margins as M
 import pytest
 
 import wbc_ref as R
@@ -13,8 +15,8 @@ from quadrupedwholebodycontroller_amd import STATELESS, Engine, default_params, 
 pytestmark = pytest.mark.gpu
 
 
-def close(a, b, tol):
-    return np.max(np.abs(a - b)) <= tol * (1.0 + np.max(np.abs(b)))
+def close(a, b, tol, quantity="value"):
+    return M.close(a, b, tol, quantity)
 
 
 @pytest.mark.parametrize("mu", [0.35, 0.6, 1.5])
@@ -35,5 +37,5 @@ def test_friction_coefficient_matches_oracle(mu, gen):
     ok = o["status"] == 0
     assert ok.sum() > B // 2
     for b in np.nonzero(ok)[0]:
-        assert close(out["tau"][b], o["tau"][b], 1e-7), (mu, gen, b)
-        assert close(out["grf"][b], o["grf"][b], 1e-7), (mu, gen, b)
+        assert close(out["tau"][b], o["tau"][b], 1e-7, "tau"), (mu, gen, b)
+        assert close(out["grf"][b], o["grf"][b], 1e-7, "grf"), (mu, gen, b)

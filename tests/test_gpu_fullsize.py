@@ -9,14 +9,14 @@ per pass); the smaller parity tests fit in one.  Each test runs the full batch o
     method, the 12-variable form the default step solves), x* / tau at the tolerances of
     test_gpu_parity.py;
   * re-runs the sampled rows as a small batch and requires bit-identical outputs (a robot's
-    result does not depend on where in the grid, or in which pass, it ran).  One exception: a
-    mask-15 robot takes the four-contact stance form when its wave's four robots all have mask 15
-    and the general 12-variable form otherwise, so where resampling changes its
-    neighbours it agrees to rounding instead (status equal, iterations but for near-ties).
+    result does not depend on where in the grid, in which pass or next to which robots it ran: each
+    QP's form follows from its own mask, and the wave map only decides who shares a wave,
+    DESIGN.md 4.11).
 """
 import numpy as np
 import pytest
 
+import margins as M
 import wbc_ref as R
 from quadrupedwholebodycontroller_amd import STATELESS, Engine, workloads
 
@@ -52,13 +52,12 @@ def check_vs_oracle(out, rows, inp_rows):
     red = R.run_batch(inp_rows, method=R.REDUCED)
     assert np.array_equal(out["status"][rows], o["status"])
     same_it = out["iters"][rows] == red["iters"]
-    assert same_it.mean() >= 0.99, int((~same_it).sum())
+    assert M.record("iters mismatch fraction", 1.0 - same_it.mean(), 0.01) <= 0.01, int((~same_it).sum())
     ok = o["status"] == 0
     for j in np.nonzero(ok)[0]:
         b = rows[j]
-        x = o["x"][j]
-        assert np.max(np.abs(out["x"][b] - x)) <= 1e-8 * (1 + np.max(np.abs(x))), (b, "x")
-        assert np.max(np.abs(out["tau"][b] - o["tau"][j])) <= 1e-7 * (1 + np.max(np.abs(o["tau"][j]))), (b, "tau")
+        assert M.close(out["x"][b], o["x"][j], 1e-8, "x"), (b, "x")
+        assert M.close(out["tau"][b], o["tau"][j], 1e-7, "tau"), (b, "tau")
 
 
 @pytest.mark.parametrize("name,B,seed", [("stance_cold", 4096, 1), ("rl_random", 8192, 3)])
@@ -70,17 +69,8 @@ def test_full_batch_sample_matches_oracle_and_small_batch(name, B, seed):
     sub = {k: np.ascontiguousarray(v[rows]) for k, v in inp.items()}
     check_vs_oracle(out, rows, sub)
     small = run(sub)
-    full15 = (inp["contacts"] == 15).reshape(-1, 4).all(1).repeat(4)[rows]
-    pad = (-len(rows)) % 4
-    sub15 = np.concatenate([sub["contacts"], np.full(pad, sub["contacts"][-1])]).reshape(-1, 4)
-    sub15 = (sub15 == 15).all(1).repeat(4)[:len(rows)]
-    same_form = full15 == sub15
     for k in KEYS:
-        assert np.array_equal(small[k][same_form], out[k][rows][same_form]), k
-    d = ~same_form
-    assert np.array_equal(small["status"][d], out["status"][rows][d])
-    for k in ("tau", "x"):
-        assert np.max(np.abs(small[k][d] - out[k][rows][d]), initial=0.0) <= 1e-10 * (1 + np.max(np.abs(out[k]))), k
+        assert np.array_equal(small[k], out[k][rows]), k
 
 
 def test_modes_full_shard_sample_matches_oracle_and_small_batch():

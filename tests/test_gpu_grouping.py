@@ -16,6 +16,8 @@ robot's outputs depend only on its own inputs, mask and flags, never on which ro
 The reference solves one robot per call (cpp:650-652), so any dependence on batch neighbours would
 be an artefact of batching."""
 import numpy as np
+
+import margins as M
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -137,6 +139,4 @@ def test_grouped_step_matches_oracle():
     a = run(inp)
     assert np.array_equal(a["status"], o["status"])
     ok = a["status"] == 0
-    err = np.max(np.abs(a["tau"][ok] - o["tau"][ok]))
-    print(f"grouped rl_random B=640: max |tau - oracle| = {err:.3e} N m")
-    assert err < 1e-7
+    assert M.close(a["tau"][ok], o["tau"][ok], 1e-7, "tau")

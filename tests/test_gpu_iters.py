@@ -26,6 +26,8 @@ full steps, so they visit the same working sets:
     the same warm start, status and iterations agree step by step, also under a lowered cap.
 """
 import numpy as np
+
+import margins as M
 import pytest
 
 import wbc_ref as R
@@ -79,7 +81,8 @@ def test_cold_iterations_match_oracle(case, path):
     lit = o if method == R.LITERAL else R.run_batch(inp, **ov)
     assert np.array_equal(g["status"], o["status"]) and np.array_equal(g["status"], lit["status"]), case
     same = g["iters"] == o["iters"]
-    assert same.mean() >= frac, (case, int((~same).sum()), np.unique(g["iters"] - o["iters"], return_counts=True))
+    assert M.record("iters mismatch fraction", 1.0 - same.mean(), 1.0 - frac) <= 1.0 - frac + 1e-12, \
+        (case, int((~same).sum()), np.unique(g["iters"] - o["iters"], return_counts=True))
     ok = lit["status"] == 0
     assert np.max(np.abs(g["tau"][ok] - lit["tau"][ok])) <= 1e-7 * (1 + np.max(np.abs(lit["tau"][ok])))
 
@@ -104,9 +107,11 @@ def test_max_iter_status_matches_oracle(case, max_wsr, path):
     assert hit.any() and (~hit).any(), "cap must split the batch"
     mism = np.nonzero(g["status"] != o["status"])[0]
     # a near-tie robot may take another route (see above); never more than 1 %
-    assert len(mism) <= max(1, len(inp["contacts"]) // 100), (case, max_wsr, mism[:10])
+    lim = max(1, len(inp["contacts"]) // 100)
+    assert M.record("MAX_ITER status mismatch fraction", len(mism) / len(inp["contacts"]),
+                    lim / len(inp["contacts"])) <= lim / len(inp["contacts"]), (case, max_wsr, mism[:10])
     ok = (g["status"] == 0) & (o["status"] == 0)
-    assert np.max(np.abs(g["tau"][ok] - o["tau"][ok])) <= 1e-7 * (1 + np.max(np.abs(o["tau"][ok])))
+    assert M.close(g["tau"][ok], o["tau"][ok], 1e-7, "tau")
     # MAX_ITER publishes nothing (the loop stops, cpp:654-659): zeros, iters = the cap
     capped = g["status"] == 1
     assert np.all(g["tau"][capped] == 0.0) and np.all(g["iters"][capped] == max_wsr)

@@ -8,6 +8,8 @@ Tolerances (BASELINE.md parity gate; fp64 everywhere):
   QP status identical.
 """
 import numpy as np
+
+import margins as M
 import pytest
 
 import wbc_np as W
@@ -52,14 +54,13 @@ def check_robot(ctrl, out, b, tol_int=1e-10):
     ref = ctrl.debug_record()
     for k in ("com", "comvel", "pose", "vc", "M", "Cnu", "Jfeet", "pfeet", "vfeet", "Mbar_b", "Mbar_j", "Jbar",
               "W", "r1", "rsw"):
-        assert rel_err(d[k], ref[k]) < tol_int, (b, k, rel_err(d[k], ref[k]))
-    assert rel_err(d["bbar"][6:], ref["bbar"][6:]) < tol_int, (b, "bbar")
+        assert M.record(k, rel_err(d[k], ref[k]), tol_int) < tol_int, (b, k, rel_err(d[k], ref[k]))
+    assert M.record("bbar", rel_err(d["bbar"][6:], ref["bbar"][6:]), tol_int) < tol_int, (b, "bbar")
     assert out["status"][b] == ctrl.qp_status, (b, out["status"][b], ctrl.qp_status)
     if ctrl.qp_status == W.QP_OK:
-        x = ctrl.qp_solution
-        assert np.max(np.abs(out["x"][b] - x)) <= 1e-8 * (1 + np.max(np.abs(x))), (b, "x")
-        assert np.max(np.abs(out["tau"][b] - ctrl.tau)) <= 1e-7 * (1 + np.max(np.abs(ctrl.tau))), (b, "tau")
-        assert np.max(np.abs(out["grf"][b] - ctrl.grf)) <= 1e-8 * (1 + np.max(np.abs(ctrl.grf))), (b, "grf")
+        assert M.close(out["x"][b], ctrl.qp_solution, 1e-8, "x"), (b, "x")
+        assert M.close(out["tau"][b], ctrl.tau, 1e-7, "tau"), (b, "tau")
+        assert M.close(out["grf"][b], ctrl.grf, 1e-8, "grf"), (b, "grf")
 
 
 def test_stance_cold_parity():

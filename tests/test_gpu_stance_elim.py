@@ -20,6 +20,8 @@ src/whole_body_controller.cpp:466-535, so:
     per-row all-stance step through the same (stance kernel) solve.
 """
 import numpy as np
+
+import margins as M
 import pytest
 import torch
 
@@ -50,8 +52,8 @@ def run(inp, bind_contacts=False, split=False, params=None):
     return out
 
 
-def close(a, b, tol):
-    return np.max(np.abs(a - b)) <= tol * (1.0 + np.max(np.abs(b)))
+def close(a, b, tol, quantity="value"):
+    return M.close(a, b, tol, quantity)
 
 
 def test_stance_path_equals_general_path():
@@ -65,9 +67,9 @@ def test_stance_path_equals_general_path():
         n = len(other["status"])
         assert np.array_equal(elim["status"][:n], other["status"])
         assert np.array_equal(elim["iters"][:n], other["iters"])
-        assert close(elim["tau"][:n], other["tau"], 1e-9)
-        assert close(elim["grf"][:n], other["grf"], 1e-9)
-        assert close(elim["x"][:n], other["x"], 1e-8)
+        assert close(elim["tau"][:n], other["tau"], 1e-9, "tau")
+        assert close(elim["grf"][:n], other["grf"], 1e-9, "grf")
+        assert close(elim["x"][:n], other["x"], 1e-8, "x")
 
 
 @pytest.mark.parametrize("maker,B", [("stance_cold", 4096), ("stance_cold", 333)])
@@ -76,10 +78,11 @@ def test_inline_solve_equals_stance_kernel(maker, B):
     inl = run(inp)
     ker = run(inp, split=True)
     assert np.array_equal(inl["status"], ker["status"])
-    assert (inl["iters"] == ker["iters"]).mean() >= 0.995
+    assert M.record("iters mismatch fraction (inline vs stance kernel)",
+                    1.0 - (inl["iters"] == ker["iters"]).mean(), 0.005) <= 0.005
     assert (inl["status"] == 0).mean() > 0.9
     for k in ("tau", "grf", "x"):
-        assert close(inl[k], ker[k], 1e-11), k
+        assert close(inl[k], ker[k], 1e-11, k), k
 
 
 @pytest.mark.parametrize("max_torque,seed", [(80.0, 61), (20.0, 62), (6.0, 63)])
@@ -106,14 +109,16 @@ def test_stance_stress_inline_matches_oracle(max_torque, seed):
     # route of different length to the same optimum under different rounding (test_gpu_iters.py)
     # (stress inputs: many feet at zero force, so many near-ties; the solutions are checked below)
     same_k, same_o = (inl["iters"] == ker["iters"]).mean(), (inl["iters"] == o["iters"]).mean()
+    M.record("iters mismatch fraction (inline vs stance kernel)", 1.0 - same_k, 0.10)
+    M.record("iters mismatch fraction (inline vs oracle)", 1.0 - same_o, 0.10)
     assert same_k >= 0.90 and same_o >= 0.90, (same_k, same_o)
     ok = o["status"] == 0
     assert ok.sum() > 0 and inl["iters"][ok].max() > 8
     if max_torque < 10.0:
         assert ok.sum() < B
     for b in np.nonzero(ok)[0]:
-        assert close(inl["tau"][b], o["tau"][b], 1e-7), b
-        assert close(inl["x"][b], o["x"][b], 1e-8), b
+        assert close(inl["tau"][b], o["tau"][b], 1e-7, "tau"), b
+        assert close(inl["x"][b], o["x"][b], 1e-8, "x"), b
 
 
 @pytest.mark.parametrize("max_wsr", [1, 2, 3])
@@ -131,7 +136,7 @@ def test_inline_max_iter_matches_oracle(max_wsr):
     assert np.all(out["iters"][capped] == max_wsr)
     assert np.all(out["tau"][capped] == 0.0) and np.all(out["x"][capped] == 0.0)
     for b in np.nonzero(o["status"] == 0)[0]:
-        assert close(out["tau"][b], o["tau"][b], 1e-7), b
+        assert close(out["tau"][b], o["tau"][b], 1e-7, "tau"), b
 
 
 def test_straight_knee_falls_back_and_matches_oracle():
@@ -145,8 +150,8 @@ def test_straight_knee_falls_back_and_matches_oracle():
     ok = o["status"] == 0
     assert ok.sum() >= B // 2
     for b in np.nonzero(ok)[0]:
-        assert close(out["tau"][b], o["tau"][b], 1e-7), b
-        assert close(out["x"][b], o["x"][b], 1e-8), b
+        assert close(out["tau"][b], o["tau"][b], 1e-7, "tau"), b
+        assert close(out["x"][b], o["x"][b], 1e-8, "x"), b
     # and the bent robots of the same batch are unaffected by their straight-legged neighbours
     inp2 = {k: v.copy() for k, v in inp.items()}
     inp2["qj"] = bent

@@ -14,6 +14,8 @@ x and tau (same bound as tests/test_oracles.py); QP status identical.
 import os
 
 import numpy as np
+
+import margins as M
 import pytest
 
 import wbc_ref as R
@@ -28,9 +30,8 @@ def load(name):
     return dict(np.load(os.path.join(GOLDEN, name + ".npz")))
 
 
-def close_to(a, b, tol):
-    a, b = np.asarray(a), np.asarray(b)
-    return np.max(np.abs(a - b)) <= tol * (1 + np.max(np.abs(b)))
+def close_to(a, b, tol, quantity="value"):
+    return M.close(a, b, tol, quantity)
 
 
 def run_cold(inp):
@@ -51,8 +52,8 @@ def test_cold_golden_fixtures(name):
     out = run_cold(inp)
     assert np.array_equal(out["status"], g["out_status"]), name
     for b in np.nonzero(g["out_status"] == 0)[0]:
-        assert close_to(out["x"][b], g["out_x"][b], 1e-8), (name, b, "x")
-        assert close_to(out["tau"][b], g["out_tau"][b], 1e-9), (name, b, "tau")
+        assert close_to(out["x"][b], g["out_x"][b], 1e-8, "x"), (name, b, "x")
+        assert close_to(out["tau"][b], g["out_tau"][b], 1e-9, "tau"), (name, b, "tau")
 
 
 @pytest.mark.parametrize("name", ["traj_stance_hold", "traj_trot"])
@@ -68,8 +69,8 @@ def test_stateful_trajectory_golden(name):
         assert np.array_equal(o["status"], g["out_status"][t]), t
         for j in range(nr):
             if g["out_status"][t, j] == 0:
-                assert close_to(o["x"][j], g["out_x"][t, j], 1e-7), (t, j, "x")
-                assert close_to(o["tau"][j], g["out_tau"][t, j], 1e-7), (t, j, "tau")
+                assert close_to(o["x"][j], g["out_x"][t, j], 1e-7, "x"), (t, j, "x")
+                assert close_to(o["tau"][j], g["out_tau"][t, j], 1e-7, "tau"), (t, j, "tau")
     e.close()
 
 
@@ -94,8 +95,8 @@ def test_stateful_trot_batch_vs_c_oracle():
                                int(inp["contacts"][j]), int(inp["switching"][j]))
             assert o["status"][j] == r["status"], (t, j)
             if r["status"] == 0:
-                assert close_to(o["tau"][j], r["tau"], 1e-7), (t, j)
-                assert close_to(o["x"][j], r["x"], 1e-7), (t, j)
+                assert close_to(o["tau"][j], r["tau"], 1e-7, "tau"), (t, j)
+                assert close_to(o["x"][j], r["x"], 1e-7, "x"), (t, j)
                 n_checked += 1
     e.close()
     assert n_checked > B * steps // 2
@@ -122,7 +123,7 @@ def test_reset_mask_restarts_selected_robots():
                                int(inp["contacts"][j]), int(inp["switching"][j]))
             assert o["status"][j] == r["status"], (t, j)
             if r["status"] == 0:
-                assert close_to(o["tau"][j], r["tau"], 1e-7), (t, j)
+                assert close_to(o["tau"][j], r["tau"], 1e-7, "tau"), (t, j)
     e.close()
 
 
@@ -134,8 +135,8 @@ def test_ragged_batches_vs_c_oracle(B):
     assert np.array_equal(out["status"], ref["status"])
     ok = ref["status"] == 0
     for b in np.nonzero(ok)[0]:
-        assert close_to(out["x"][b], ref["x"][b], 1e-8), b
-        assert close_to(out["tau"][b], ref["tau"][b], 1e-9), b
+        assert close_to(out["x"][b], ref["x"][b], 1e-8, "x"), b
+        assert close_to(out["tau"][b], ref["tau"][b], 1e-9, "tau"), b
 
 
 def test_nonfinite_input_is_isolated():
@@ -149,7 +150,7 @@ def test_nonfinite_input_is_isolated():
     good = np.setdiff1d(np.arange(128), bad)
     ref = R.run_batch({k: v[good] for k, v in inp.items()})
     assert np.array_equal(out["status"][good], ref["status"])
-    assert close_to(out["tau"][good], ref["tau"], 1e-9)
+    assert close_to(out["tau"][good], ref["tau"], 1e-9, "tau")
 
 
 def test_device_bound_inputs_and_outputs():
@@ -213,8 +214,8 @@ def test_hotstart_same_solution_fewer_iterations():
         oh, oc = hot.outputs(), cold.outputs()
         assert np.array_equal(oh["status"], oc["status"]), t
         ok = oc["status"] == 0
-        assert close_to(oh["tau"][ok], oc["tau"][ok], 1e-9), t
-        assert close_to(oh["x"][ok], oc["x"][ok], 1e-9), t
+        assert close_to(oh["tau"][ok], oc["tau"][ok], 1e-9, "tau"), t
+        assert close_to(oh["x"][ok], oc["x"][ok], 1e-9, "x"), t
         if t > 0:
             it_hot += int(oh["iters"].sum())
             it_cold += int(oc["iters"].sum())
@@ -243,8 +244,8 @@ def test_stateful_trot_with_stretched_legs_vs_c_oracle():
                                int(inp["contacts"][j]), int(inp["switching"][j]))
             assert o["status"][j] == r["status"], (t, j)
             if r["status"] == 0:
-                assert close_to(o["tau"][j], r["tau"], 1e-7), (t, j)
-                assert close_to(o["x"][j], r["x"], 1e-7), (t, j)
+                assert close_to(o["tau"][j], r["tau"], 1e-7, "tau"), (t, j)
+                assert close_to(o["x"][j], r["x"], 1e-7, "x"), (t, j)
                 n_checked += 1
     e.close()
     assert n_checked > B * steps // 2
