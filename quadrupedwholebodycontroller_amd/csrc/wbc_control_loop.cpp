@@ -144,12 +144,20 @@ int run_node(long cycles) {
         if (it + 1 >= cycles) wbc.requestShutdown();  // ros::shutdown: this cycle is the last
     };
     const long n = wbc.run();
-    const auto& tau = wbc.jointTorques();
-    std::printf("{\"config\": \"node_run\", \"cycles\": %ld, \"qp_status\": %d, \"messages\": %ld, \"tau\": [", n,
-                wbc.qpReturnValue(), sent.load());
+    const auto tau = wbc.jointTorques();  // (a copy: the loop below publishes new torques)
+    const int status = wbc.qpReturnValue();
+    // after run() ended by requestShutdown(), a direct controlLoop() starts with ok() true again
+    // (the shutdown request belonged to the finished loop) and runs its own cycles
+    const long again = wbc.controlLoop(25, 0.0, [&](long) {
+        wbc.floatingBaseStateCallback(ms);
+        wbc.jointStateCallback(js);
+        wbc.referenceCallback(rm);
+    });
+    std::printf("{\"config\": \"node_run\", \"cycles\": %ld, \"control_loop_after_run\": %ld, \"qp_status\": %d, "
+                "\"messages\": %ld, \"tau\": [", n, again, status, sent.load());
     for (int i = 0; i < numberOfJoints; ++i) std::printf("%s%.9g", i ? ", " : "", tau[i]);
     std::printf("]}\n");
-    return wbc.qpReturnValue() == WBC_QP_OK ? 0 : 3;
+    return status == WBC_QP_OK && wbc.qpReturnValue() == WBC_QP_OK ? 0 : 3;
 }
 
 int run_replay(const char* in_path, const char* out_path) {

@@ -174,23 +174,6 @@ wbc::KernelArgs make_args(wbc_engine* h, uint32_t flags) {
 hipError_t upload_qmap(wbc_engine* h, const uint8_t* masks) {
     h->qmap_waves = wbc::qmap_build(masks, h->batch, h->h_qmap);
     h->qmap_host = true;
-#ifdef WBC_DIAG_MAP  // (A/B diagnostics only) 1: identity order through the map, 2: a fixed shuffle
-    {
-        const int B = h->batch;
-        uint64_t x = 88172645463325252ull;
-        for (int i = 0; i < B; ++i) h->h_qmap[i] = i;
-        if (WBC_DIAG_MAP == 2)
-            for (int i = B - 1; i > 0; --i) {
-                x ^= x << 13; x ^= x >> 7; x ^= x << 17;
-                const int j = (int)(x % (uint64_t)(i + 1));
-                const int t = h->h_qmap[i]; h->h_qmap[i] = h->h_qmap[j]; h->h_qmap[j] = t;
-            }
-        for (int i = 0; i < B; ++i) h->h_qmap[i] = wbc::qmap_entry(h->h_qmap[i], masks[h->h_qmap[i]]);
-        int w = (B + 3) / 4;
-        for (int i = B; i < 4 * w; ++i) h->h_qmap[i] = ~wbc::qmap_entry(B - 1, masks[B - 1]);
-        h->qmap_waves = w;
-    }
-#endif
     if (!h->qmap_waves) return hipSuccess;
     return hipMemcpyAsync(h->d_qmap, h->h_qmap, (size_t)h->qmap_waves * wbc::QMAP_SEG * sizeof(int32_t),
                           hipMemcpyHostToDevice, h->stream);

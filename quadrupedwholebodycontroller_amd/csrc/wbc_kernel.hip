@@ -503,8 +503,10 @@ __device__ __forceinline__ double atan2_br(double y, double x) {
                               -1.99999999998764832476e-01);
     const double at = hi - ((u * (s1 + s2) - lo) - u);  // atan t
     double r = (ay > ax) ? 1.57079632679489655800e+00 - at : at;
-    r = (x < 0.0) ? 3.14159265358979311600e+00 - r : r;
-    return (y < 0.0) ? -r : r;
+    // quadrant from the sign bits (as std::atan2: atan2(+-0, x < 0) = +-pi, atan2(+-0, -0) = +-pi);
+    // a comparison with 0.0 would treat -0 as +0 and return +pi for y = -0
+    r = signbit(x) ? 3.14159265358979311600e+00 - r : r;
+    return signbit(y) ? -r : r;
 }
 __device__ __forceinline__ double sel3(const double* v, int k) { return k == 0 ? v[0] : (k == 1 ? v[1] : v[2]); }
 __device__ __forceinline__ double sel4d(int k, double a, double b, double c, double d) {
@@ -846,9 +848,13 @@ __device__ bool stance_reduce([[maybe_unused]] const KernelArgs& ka, [[maybe_unu
     // S^-1 by Gauss-Jordan without pivoting (S is well conditioned: cond < 10 on the bench and
     // stress states, smallest pivot > 0.25 max|S|; a pivot below 1e-6 max|S| takes the general
     // path), row r in lane r < 6, pivot rows broadcast with DPP row_newbcast
+    // Row r of S^-1 (ir) and z_r = S[r][6] stay in lane r's registers for the Y rows below, which
+    // take them by DPP broadcast (LDS reads of S^-1 there waited ~19 times)
+    double ir[6], zr;
     {
         const int r = lane < 6 ? lane : 5;
-        double sr_[6], ir[6];
+        double sr_[6];
+        zr = R.S[r][6];
 #pragma unroll
         for (int c = 0; c < 6; ++c) {
             sr_[c] = R.S[r][c];
@@ -875,10 +881,6 @@ __device__ bool stance_reduce([[maybe_unused]] const KernelArgs& ka, [[maybe_unu
         }
         ok = ok && pmin > 1e-6 * smx;
         UST(ka, rb, 12);  // leg inverses, S, S^-1
-        if (lane < 6) {
-#pragma unroll
-            for (int c = 0; c < 6; ++c) R.Si[lane][c] = ir[c];
-        }
     }
     ok = !seg_any<16>(!ok);  // every leg and S usable (uniform over the robot)
     lds_sync();
@@ -893,9 +895,9 @@ __device__ bool stance_reduce([[maybe_unused]] const KernelArgs& ka, [[maybe_unu
         for (int c = 0; c < 6; ++c) {
             double a4[2] = {0.0, 0.0};
 #pragma unroll
-            for (int t = 0; t < 6; ++t) a4[t & 1] = fma(wrow[t], R.Si[t][c], a4[t & 1]);
+            for (int t = 0; t < 6; ++t) a4[t & 1] = fma(wrow[t], seg_bcast<16>(ir[c], t), a4[t & 1]);
             yi[c] = a4[0] + a4[1];
-            q = fma(yi[c], R.S[c][6], q);
+            q = fma(yi[c], seg_bcast<16>(zr, c), q);
         }
         if (lane < 12) {
 #pragma unroll
@@ -1383,9 +1385,12 @@ __device__ bool reduce_general([[maybe_unused]] const KernelArgs& ka, [[maybe_un
     }
     lds_sync();
     // R3: S6^-1 by Gauss-Jordan without pivoting (S6 = I without stance legs; cond < 10 otherwise)
+    // (row r of S6^-1 and z6_r stay in lane r's registers: R4 takes them by DPP broadcast)
+    double ir[6], zr;
     {
         const int r = lane < 6 ? lane : 5;
-        double sr_[6], ir[6];
+        double sr_[6];
+        zr = R.S[r][6];
 #pragma unroll
         for (int c = 0; c < 6; ++c) {
             sr_[c] = R.S[r][c];
@@ -1411,10 +1416,6 @@ __device__ bool reduce_general([[maybe_unused]] const KernelArgs& ka, [[maybe_un
             for (int c = 0; c <= kk; ++c) ir[c] = fma(-f, prow[6 + c], ir[c] * own);
         }
         ok = ok && pmin > 1e-6 * smx;
-        if (lane < 6) {
-#pragma unroll
-            for (int c = 0; c < 6; ++c) R.Si[lane][c] = ir[c];
-        }
     }
     ok = !seg_any<16>(!ok);
     lds_sync();
@@ -1427,18 +1428,26 @@ __device__ bool reduce_general([[maybe_unused]] const KernelArgs& ka, [[maybe_un
 #pragma unroll
         for (int c = 0; c < 6; ++c) wrow[c] = R.W[i][c];
         q = R.w[i];
-#pragma unroll
-        for (int c = 0; c < 6; ++c) {
-            double a4[2] = {0.0, 0.0};
-#pragma unroll
-            for (int t = 0; t < 6; ++t) a4[t & 1] = fma(wrow[t], R.Si[t][c], a4[t & 1]);
-            yi[c] = a4[0] + a4[1];
-            q = fma(yi[c], R.S[c][6], q);
-        }
         double pkv[3];
         pk3(k, dl, pkv);
 #pragma unroll
         for (int c = 0; c < 3; ++c) { Ei[c] = (c == k) ? 1.0 : 0.0; Ei[3 + c] = pkv[c]; }
+        // Y_i = W_i S6^-1 and (S6^-T E_i^T)_c = sum_b S6^-1[b][c] E_i[b] in one pass over the
+        // broadcast entries of S6^-1 (no LDS round trip)
+        double sv[6];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+            double a4[2] = {0.0, 0.0}, tv = 0.0;
+#pragma unroll
+            for (int t = 0; t < 6; ++t) {
+                const double sb = seg_bcast<16>(ir[c], t);
+                a4[t & 1] = fma(wrow[t], sb, a4[t & 1]);
+                tv = fma(sb, Ei[t], tv);
+            }
+            yi[c] = a4[0] + a4[1];
+            sv[c] = tv;
+            q = fma(yi[c], seg_bcast<16>(zr, c), q);
+        }
         double Ki[6];
 #pragma unroll
         for (int c = 0; c < 3; ++c) { Ki[c] = s.A[i][c] * inv_m; Ki[3 + c] = s.KA[i][c]; }
@@ -1456,12 +1465,7 @@ __device__ bool reduce_general([[maybe_unused]] const KernelArgs& ka, [[maybe_un
         // swing row: v_i = -S6^-T E_i^T, rho0_i = E_i c_psi - rsw_i
         double vi[6];
 #pragma unroll
-        for (int c = 0; c < 6; ++c) {
-            double t = 0.0;
-#pragma unroll
-            for (int b = 0; b < 6; ++b) t = fma(R.Si[b][c], Ei[b], t);
-            vi[c] = sti ? yi[c] : -t;
-        }
+        for (int c = 0; c < 6; ++c) vi[c] = sti ? yi[c] : -sv[c];
         double ec = 0.0;
 #pragma unroll
         for (int c = 0; c < 6; ++c) ec = fma(Ei[c], cpsi[c], ec);
@@ -1588,7 +1592,8 @@ __device__ bool reduce_general([[maybe_unused]] const KernelArgs& ka, [[maybe_un
         for (int kk = 0; kk < 12; ++kk) {
             const double mk = P.Mbj[r * 12 + kk];
             const bool stk = (kap >> (kk / 3)) & 1;
-            const double jc = stk ? P.Jbj[kk * 12 + r] : 0.0;
+            const double jcv = P.Jbj[kk * 12 + r];  // loaded, then masked (no load under the mask branch)
+            const double jc = stk ? jcv : 0.0;
             mrow[kk] = stk ? jc : -mk;  // the slot's own term of Nt[r][kk]
 #pragma unroll
             for (int c = 0; c < 6; ++c) my[c] = fma(mk, R.Y[kk][c], my[c]);
@@ -2444,14 +2449,14 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
         double Al[3] = {0, 0, 0}, Aa[3] = {0, 0, 0}, hsum[3] = {0, 0, 0}, Mrow[3] = {0, 0, 0};
         // every lane runs the three bodies of its leg, the ones above its joint weighted by 0: a
         // lane-dependent `if (kk >= k)` put each body's LDS loads in an exec-masked block with its
-        // own wait (SUB = 16; the 64-lane kernel keeps the branch, its registers are tighter)
+        // own wait
 #pragma unroll
         for (int kk = 0; kk < 3; ++kk) {
             const bool below = kk >= k;
-            if (SUB == 16 || below) {
+            {
                 const int b = 1 + 3 * l + kk;
-                const double mb = (SUB == 16 && !below) ? 0.0 : md.link[l][kk].mass;
-                const double wI = (SUB == 16 && !below) ? 0.0 : 1.0;  // the inertia and force terms
+                const double mb = below ? md.link[l][kk].mass : 0.0;
+                const double wI = below ? 1.0 : 0.0;  // the inertia and force terms
                 const Body& bd = s.bd[b];
                 const double cb[3] = {bd.c[0], bd.c[1], bd.c[2]};
                 double rel[3] = {cb[0] - oj[0], cb[1] - oj[1], cb[2] - oj[2]}, v[3], t[3], Ia[3], fm[3];
@@ -2589,7 +2594,7 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
     // dt (an IEEE division is ~10 dependent instructions; the two agree to an ulp)
     const double rdt = pr.loop_rate;
 
-    if constexpr (SUB == 64) {  // the fused kernel (2 waves per SIMD): stores in the loops, no spills
+    if constexpr (SUB == 64) {  // the fused kernel (2 waves per SIMD): stores in the loops (no spills)
       if (lane < 12) {
         const int j = lane, lj = j / 3, kj = j % 3;
         const double Alj[3] = {s.A[j][0], s.A[j][1], s.A[j][2]}, Aaj[3] = {s.A[j][3], s.A[j][4], s.A[j][5]};
@@ -2879,11 +2884,7 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
         // on stateful steps).  The choice is the segment's own, so a QP's result never depends on
         // its wave-mates; the wave map (KernelArgs::qmap) gives every wave one mask, so the branch
         // does not diverge (a mixed wave, from unmapped device-bound masks, runs both forms)
-#ifndef WBC_WAVE_FORM
         if (!stateful && kap == 15) {
-#else  // (A/B diagnostics only: the form chosen per wave, as before the wave map)
-        if (!stateful && __all(kap == 15)) {
-#endif
             double hrow[12], gsv = 0.0;
             if (stance_reduce<true>(a, rb, P, pr, lane, wr, s, hrow, gsv, nullptr) && rank6_factor(P, s, gsv, lane)) {
                 UST(a, rb, 11);

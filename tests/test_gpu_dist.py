@@ -4,7 +4,7 @@ tau | status | iters into its StepOutputs block and the blocks are gathered
 (sharding.gather_step_outputs, the code bench.py runs over RCCL).  Rank 0 checks the gathered batch
 against one full-batch engine run on the same device (bit-identical on both batches: the step groups
 its QPs by contact mask, so a robot's result does not depend on the shard boundary) and against the C oracle (status equal,
-tau to 1e-7) for a batch over all 16 contact masks.  The reference's own step is per robot
+tau to 1e-9, tests/margins.py TAU) for a batch over all 16 contact masks.  The reference's own step is per robot
 (cpp:650-652), so sharding robots across ranks is exact."""
 import os
 import subprocess
@@ -55,7 +55,7 @@ for name, inp in (("stance", workloads.stance_cold(1031, seed=5)), ("rl_random",
         assert np.array_equal(st, o["status"]), name
         ok = st == 0
         err = np.max(np.abs(tau[ok] - o["tau"][ok])) / (1.0 + np.max(np.abs(o["tau"][ok])))
-        assert err < 1e-7, (name, err)
+        assert err < 1e-9, (name, err)
         print("CHECKED", name, B, float(err), flush=True)
 print("DIST_OK", rank, flush=True)
 dist.destroy_process_group()

@@ -52,6 +52,6 @@ def test_alternating_stance_and_mixed_steps_match_oracle(split):
         ok = o["status"] == 0
         assert ok.sum() >= B // 2, (t, name)
         for b in np.nonzero(ok)[0]:
-            assert close(g["tau"][b], o["tau"][b], 1e-7, "tau"), (t, name, b)
-            assert close(g["grf"][b], o["grf"][b], 1e-7, "grf"), (t, name, b)
+            assert close(g["tau"][b], o["tau"][b], M.TAU, "tau"), (t, name, b)
+            assert close(g["grf"][b], o["grf"][b], M.GRF, "grf"), (t, name, b)
     e.close()

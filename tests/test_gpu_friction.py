@@ -37,5 +37,5 @@ def test_friction_coefficient_matches_oracle(mu, gen):
     ok = o["status"] == 0
     assert ok.sum() > B // 2
     for b in np.nonzero(ok)[0]:
-        assert close(out["tau"][b], o["tau"][b], 1e-7, "tau"), (mu, gen, b)
-        assert close(out["grf"][b], o["grf"][b], 1e-7, "grf"), (mu, gen, b)
+        assert close(out["tau"][b], o["tau"][b], M.TAU, "tau"), (mu, gen, b)
+        assert close(out["grf"][b], o["grf"][b], M.GRF, "grf"), (mu, gen, b)

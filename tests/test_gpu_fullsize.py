@@ -56,8 +56,8 @@ def check_vs_oracle(out, rows, inp_rows):
     ok = o["status"] == 0
     for j in np.nonzero(ok)[0]:
         b = rows[j]
-        assert M.close(out["x"][b], o["x"][j], 1e-8, "x"), (b, "x")
-        assert M.close(out["tau"][b], o["tau"][j], 1e-7, "tau"), (b, "tau")
+        assert M.close(out["x"][b], o["x"][j], M.X, "x"), (b, "x")
+        assert M.close(out["tau"][b], o["tau"][j], M.TAU, "tau"), (b, "tau")
 
 
 @pytest.mark.parametrize("name,B,seed", [("stance_cold", 4096, 1), ("rl_random", 8192, 3)])

@@ -11,7 +11,7 @@ robot's outputs depend only on its own inputs, mask and flags, never on which ro
   its own form), also on a permuted batch.
 * Mask-15 robots in a mixed stateless batch take the four-contact stance form, as in an all-stance
   batch: bit-identical to the same robots stepped alone.
-* The grouped step still matches the C oracle (status equal, tau to 1e-7) on every mask.
+* The grouped step still matches the C oracle (status equal, tau to margins.TAU) on every mask.
 
 The reference solves one robot per call (cpp:650-652), so any dependence on batch neighbours would
 be an artefact of batching."""
@@ -139,4 +139,4 @@ def test_grouped_step_matches_oracle():
     a = run(inp)
     assert np.array_equal(a["status"], o["status"])
     ok = a["status"] == 0
-    assert M.close(a["tau"][ok], o["tau"][ok], 1e-7, "tau")
+    assert M.close(a["tau"][ok], o["tau"][ok], M.TAU, "tau")

@@ -84,7 +84,7 @@ def test_cold_iterations_match_oracle(case, path):
     assert M.record("iters mismatch fraction", 1.0 - same.mean(), 1.0 - frac) <= 1.0 - frac + 1e-12, \
         (case, int((~same).sum()), np.unique(g["iters"] - o["iters"], return_counts=True))
     ok = lit["status"] == 0
-    assert np.max(np.abs(g["tau"][ok] - lit["tau"][ok])) <= 1e-7 * (1 + np.max(np.abs(lit["tau"][ok])))
+    assert M.close(g["tau"][ok], lit["tau"][ok], M.TAU, "tau")
 
 
 CAPS = {"stance": [1, 2, 3], "rl_random": [2, 4, 8], "stress20": [5, 10, 15]}
@@ -111,7 +111,7 @@ def test_max_iter_status_matches_oracle(case, max_wsr, path):
     assert M.record("MAX_ITER status mismatch fraction", len(mism) / len(inp["contacts"]),
                     lim / len(inp["contacts"])) <= lim / len(inp["contacts"]), (case, max_wsr, mism[:10])
     ok = (g["status"] == 0) & (o["status"] == 0)
-    assert M.close(g["tau"][ok], o["tau"][ok], 1e-7, "tau")
+    assert M.close(g["tau"][ok], o["tau"][ok], M.TAU, "tau")
     # MAX_ITER publishes nothing (the loop stops, cpp:654-659): zeros, iters = the cap
     capped = g["status"] == 1
     assert np.all(g["tau"][capped] == 0.0) and np.all(g["iters"][capped] == max_wsr)
@@ -149,7 +149,7 @@ def test_hotstart_iterations_match_oracle(max_wsr, path):
             n_it += o["iters"]
             n_cap += int(o["status"] == 1)
             if o["status"] == 0 and g["status"][b] == 0:
-                assert np.max(np.abs(g["tau"][b] - o["tau"])) <= 1e-7 * (1 + np.max(np.abs(o["tau"]))), (t, b)
+                assert M.close(g["tau"][b], o["tau"], M.TAU, "tau"), (t, b)
     e.close()
     assert n_it > 0
     assert n_mism <= B * steps // 100, n_mism

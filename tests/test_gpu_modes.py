@@ -7,6 +7,8 @@ x, status and iteration counts, bit for bit.  The oracle check reuses test_gpu_p
 tolerances on a subset.
 """
 import numpy as np
+
+import margins as M
 import pytest
 
 import wbc_np as W
@@ -97,8 +99,8 @@ def test_modes_against_oracle():
             c.step()
             assert got["status"][r] == c.qp_status, (s, k)
             if c.qp_status == W.QP_OK:
-                assert np.max(np.abs(got["x"][r] - c.qp_solution)) <= 1e-8 * (1 + np.max(np.abs(c.qp_solution))), (s, k)
-                assert np.max(np.abs(got["tau"][r] - c.tau)) <= 1e-7 * (1 + np.max(np.abs(c.tau))), (s, k)
+                assert M.close(got["x"][r], c.qp_solution, M.X, "x"), (s, k)
+                assert M.close(got["tau"][r], c.tau, M.TAU, "tau"), (s, k)
 
 
 def test_no_x_and_device_outputs():

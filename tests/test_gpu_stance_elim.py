@@ -67,9 +67,9 @@ def test_stance_path_equals_general_path():
         n = len(other["status"])
         assert np.array_equal(elim["status"][:n], other["status"])
         assert np.array_equal(elim["iters"][:n], other["iters"])
-        assert close(elim["tau"][:n], other["tau"], 1e-9, "tau")
-        assert close(elim["grf"][:n], other["grf"], 1e-9, "grf")
-        assert close(elim["x"][:n], other["x"], 1e-8, "x")
+        assert close(elim["tau"][:n], other["tau"], M.SAME, "tau")
+        assert close(elim["grf"][:n], other["grf"], M.SAME, "grf")
+        assert close(elim["x"][:n], other["x"], M.SAME, "x")
 
 
 @pytest.mark.parametrize("maker,B", [("stance_cold", 4096), ("stance_cold", 333)])
@@ -82,7 +82,7 @@ def test_inline_solve_equals_stance_kernel(maker, B):
                     1.0 - (inl["iters"] == ker["iters"]).mean(), 0.005) <= 0.005
     assert (inl["status"] == 0).mean() > 0.9
     for k in ("tau", "grf", "x"):
-        assert close(inl[k], ker[k], 1e-11, k), k
+        assert close(inl[k], ker[k], M.BITS, k), k
 
 
 @pytest.mark.parametrize("max_torque,seed", [(80.0, 61), (20.0, 62), (6.0, 63)])
@@ -117,8 +117,8 @@ def test_stance_stress_inline_matches_oracle(max_torque, seed):
     if max_torque < 10.0:
         assert ok.sum() < B
     for b in np.nonzero(ok)[0]:
-        assert close(inl["tau"][b], o["tau"][b], 1e-7, "tau"), b
-        assert close(inl["x"][b], o["x"][b], 1e-8, "x"), b
+        assert close(inl["tau"][b], o["tau"][b], M.TAU, "tau"), b
+        assert close(inl["x"][b], o["x"][b], M.X, "x"), b
 
 
 @pytest.mark.parametrize("max_wsr", [1, 2, 3])
@@ -136,7 +136,7 @@ def test_inline_max_iter_matches_oracle(max_wsr):
     assert np.all(out["iters"][capped] == max_wsr)
     assert np.all(out["tau"][capped] == 0.0) and np.all(out["x"][capped] == 0.0)
     for b in np.nonzero(o["status"] == 0)[0]:
-        assert close(out["tau"][b], o["tau"][b], 1e-7, "tau"), b
+        assert close(out["tau"][b], o["tau"][b], M.TAU, "tau"), b
 
 
 def test_straight_knee_falls_back_and_matches_oracle():
@@ -150,8 +150,8 @@ def test_straight_knee_falls_back_and_matches_oracle():
     ok = o["status"] == 0
     assert ok.sum() >= B // 2
     for b in np.nonzero(ok)[0]:
-        assert close(out["tau"][b], o["tau"][b], 1e-7, "tau"), b
-        assert close(out["x"][b], o["x"][b], 1e-8, "x"), b
+        assert close(out["tau"][b], o["tau"][b], M.TAU, "tau"), b
+        assert close(out["x"][b], o["x"][b], M.X, "x"), b
     # and the bent robots of the same batch are unaffected by their straight-legged neighbours
     inp2 = {k: v.copy() for k, v in inp.items()}
     inp2["qj"] = bent

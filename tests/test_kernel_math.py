@@ -37,7 +37,7 @@ def test_trig_kernels_against_libm(tmp_path):
 #include <cmath>
 #include <cstdio>
 #include <random>
-using std::fma; using std::fabs; using std::fmax; using std::fmin;
+using std::fma; using std::fabs; using std::fmax; using std::fmin; using std::signbit;
 """ + body + r"""
 static double ulps(double a, double r) {
     const double u = std::nextafter(fabs(r), INFINITY) - fabs(r);
@@ -61,6 +61,15 @@ int main() {
     joint_sincos(3.0e5, &big_s, &big_c);  // the library path beyond |x| = 1e5
     std::printf("%.3f %.3f %.3f %d\n", es, ec, ea, big_s == std::sin(3.0e5) && big_c == std::cos(3.0e5));
     std::printf("%.17g %.17g %.17g\n", atan2_br(0.0, -1.0), atan2_br(1.0, 0.0), atan2_br(-1.0, -1.0));
+    // signed zeros (a 180-degree roll or yaw): the sign of the result follows std::atan2 bit for bit
+    const double zs[2] = {0.0, -0.0}, xs[5] = {-1.0, -0.0, 0.0, 1.0, -1e-300};
+    int bad = 0;
+    for (double yv : zs)
+        for (double xv : xs) {
+            const double a = atan2_br(yv, xv), b = std::atan2(yv, xv);
+            bad += (signbit(a) != signbit(b)) || (fabs(a - b) > 4e-16);
+        }
+    std::printf("%d\n", bad);
 }
 """)
     exe = tmp_path / "t"
@@ -73,6 +82,7 @@ int main() {
     assert float(ea) <= 2.0, ea
     assert big == "1"
     a0, a1, a2 = (float(t) for t in out[1].split())
+    assert out[2].strip() == "0", "atan2_br differs from std::atan2 on signed-zero inputs"
     assert a0 == pytest.approx(3.141592653589793, abs=1e-15)
     assert a1 == pytest.approx(1.5707963267948966, abs=1e-15)
     assert a2 == pytest.approx(-2.356194490192345, abs=1e-15)

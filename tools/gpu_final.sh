@@ -5,13 +5,14 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 TAG=${TAG:-final}
-ROUND=${ROUND:-r03}
+ROUND=${ROUND:-r04}
 O=gpurun_out/$TAG
 mkdir -p $O profiles/$ROUND
 step() { local name=$1 t=$2; shift 2; echo "== $name $(date +%T)"; timeout -k 10 $t "$@" > $O/$name.log 2>&1; local rc=$?; echo "== $name rc=$rc"; if [ $rc -ne 0 ]; then tail -30 $O/$name.log; exit $rc; fi; }
-step pytest 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+step pytest 400 env WBC_MARGINS_OUT=$O/parity_margins.json python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+cp $O/parity_margins.json profiles/$ROUND/parity_margins.json
 step smoke 120 python -c "import __graft_entry__ as g; g.smoke()"
-for cb in stance_cold_b4096:4096 rl_random_b8192:8192 modes16_b16384:16384; do
+for cb in stance_cold_b4096:4096 rl_random_b8192:8192 modes16_b16384:16384 trot_stateful_b4096:4096; do
   c=${cb%%:*}; b=${cb##*:}
   step pmc_$c 600 env TAG=${TAG}_$c CONFIG=$c BATCH=$b bash tools/pmc.sh
   cp gpurun_out/pmc_${TAG}_$c/pmc_summary.json $O/pmc_$c.json
@@ -25,6 +26,7 @@ for cb in rl_random_b8192 modes16_b16384; do
 done
 step b1_fused 120 quadrupedwholebodycontroller_amd/wbc_control_loop stance 3000 0 fused
 step b1_default 120 quadrupedwholebodycontroller_amd/wbc_control_loop stance 3000 0 default
+step b1_probe 120 python tools/b1_probe.py 2000
 step ust_stance 120 env WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_istamps.so python tools/ust16.py stance_cold 4096
 step ust_rl 120 env WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_istamps.so python tools/ust16.py rl_random 8192
 tail -1 $O/bench.log
