@@ -3,7 +3,9 @@
 // (include/anymal_wbc/whole_body_controller.hpp:106-166) with batched device buffers.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -18,6 +20,7 @@ extern "C" hipError_t wbc_launch_update(const wbc::KernelArgs* a, hipStream_t st
 extern "C" hipError_t wbc_launch_solve_general(const wbc::KernelArgs* a, hipStream_t st);
 extern "C" hipError_t wbc_launch_solve_stance(const wbc::KernelArgs* a, hipStream_t st);
 extern "C" hipError_t wbc_launch_update_solve(const wbc::KernelArgs* a, hipStream_t st);
+extern "C" hipError_t wbc_launch_modes(const wbc::KernelArgs* a, hipStream_t st);
 extern "C" hipError_t wbc_launch_reset(double* hist, const uint8_t* mask, int batch, hipStream_t st);
 extern "C" hipError_t wbc_launch_qmap(const uint8_t* masks, int batch, int32_t* map, hipStream_t st);
 
@@ -60,6 +63,12 @@ struct wbc_engine {
     // contact-mode hypotheses (wbc_set_modes): n_modes > 0 turns the inputs into B / n_modes states
     int32_t n_modes = 0;
     uint8_t* d_modes = nullptr;
+    // the update shared by mode_loop hypotheses per wave (KernelArgs::mloop; 1 = one per segment)
+    // and the hypotheses' order, chunk by chunk (plan_mode_loop)
+    int32_t mode_loop = 1;
+    uint8_t mode_order[16] = {};
+    double* d_mlbak = nullptr;  // KernelArgs::mlbak, sized for the mode loop's grid
+    size_t mlbak_len = 0;
     // bound (possibly external) inputs
     const double* in_pose = nullptr;
     const double* in_nu = nullptr;
@@ -166,6 +175,9 @@ wbc::KernelArgs make_args(wbc_engine* h, uint32_t flags) {
     a.fb_cap = h->batch;
     a.qmap = nullptr;
     a.nwaves = (h->batch + wbc::QMAP_SEG - 1) / wbc::QMAP_SEG;
+    a.mloop = 0;
+    std::memset(a.mode_order, 0, sizeof(a.mode_order));
+    a.mlbak = h->d_mlbak;
     return a;
 }
 
@@ -184,6 +196,58 @@ hipError_t upload_qmap(wbc_engine* h, const uint8_t* masks) {
 // recorded per launch: an event packet between two steps costs ~3 us of the ~36 us step (measured
 // on MI355X, 103.5 -> 112.3 M solves/s on the headline config without it).
 hipError_t drain(wbc_engine* h) { return h->stream ? hipStreamSynchronize(h->stream) : hipSuccess; }
+
+// Mode hypotheses per wave (KernelArgs::mloop, wbc_modes_kernel): the largest M dividing K that
+// still gives every SIMD of the device a wave (ceil(S / 4) K / M >= 4 CUs); 1, one hypothesis per
+// segment, when even that leaves SIMDs idle.  WBC_MODES_M (a divisor of K) overrides it (A/B runs,
+// tests).  The hypotheses go to the K / M chunks longest first, each to the chunk with the least
+// estimated work so far (LPT), so the chunks' waves end together: the estimate is a reduction and
+// solve of 30 units plus 3 per expected working-set pass (0.3, 2.3, 4.5, 6.7, 8.9
+// passes for 0 .. 4 stance legs).
+hipError_t plan_mode_loop(wbc_engine* h, const uint8_t* modes, int32_t K) {
+    const int64_t groups = (h->batch / K + 3) / 4;
+    int cus = 256;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || cus <= 0) cus = 256;
+    int M = 1;
+    for (int m = K; m > 1; --m)
+        if (K % m == 0 && groups * (K / m) >= 4LL * cus) { M = m; break; }
+    if (const char* e = std::getenv("WBC_MODES_M")) {
+        const int m = std::atoi(e);
+        if (m >= 1 && m <= K && K % m == 0) M = m;
+    }
+    static const double passes[5] = {0.3, 2.3, 4.5, 6.7, 8.9};
+    const int C = K / M;
+    int idx[16], fill[16] = {};
+    double load[16] = {};
+    for (int k = 0; k < K; ++k) idx[k] = k;
+    auto cost = [&](int k) { return 30.0 + 3.0 * passes[__builtin_popcount(modes[k] & 15)]; };
+    std::stable_sort(idx, idx + K, [&](int x, int y) { return cost(x) > cost(y); });
+    uint8_t chunk[16][16];
+    for (int t = 0; t < K; ++t) {
+        int best = -1;
+        for (int c = 0; c < C; ++c)
+            if (fill[c] < M && (best < 0 || load[c] < load[best])) best = c;
+        chunk[best][fill[best]++] = (uint8_t)idx[t];
+        load[best] += cost(idx[t]);
+    }
+    for (int c = 0; c < C; ++c)
+        for (int i = 0; i < M; ++i) h->mode_order[c * M + i] = chunk[c][i];
+    h->mode_loop = M;
+    // each segment's copy of the reduction inputs (KernelArgs::mlbak); the stream is idle here
+    const size_t need = M > 1 ? (size_t)groups * C * 4 * 288 : 0;
+    if (need > h->mlbak_len) {
+        if (h->d_mlbak) (void)hipFree(h->d_mlbak);
+        h->d_mlbak = nullptr;
+        h->mlbak_len = 0;
+        hipError_t e = hipMalloc(reinterpret_cast<void**>(&h->d_mlbak), need * sizeof(double));
+        if (e != hipSuccess) {
+            h->mode_loop = 1;  // the per-hypothesis step needs no copy
+            return e;
+        }
+        h->mlbak_len = need;
+    }
+    return hipSuccess;
+}
 
 int64_t count_stance(const uint8_t* masks, size_t n) {
     int64_t c = 0;
@@ -406,7 +470,7 @@ int32_t wbc_destroy(wbc_engine* h) {
     // which would also wait for other engines' and the caller's unrelated work)
     (void)drain(h);
     void* ptrs[] = {h->d_model, h->d_params, h->d_limg, h->d_inblk, h->d_outblk, h->d_mask, h->d_modes, h->d_hist, h->d_work,
-                    h->d_fb, h->d_dbg, h->d_qmap};
+                    h->d_fb, h->d_dbg, h->d_qmap, h->d_mlbak};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (h->h_in) (void)hipHostFree(h->h_in);
@@ -572,6 +636,7 @@ int32_t wbc_set_modes(wbc_engine* h, int32_t n_modes, const uint8_t* modes) {
     WBC_HIP(hipStreamSynchronize(h->stream));
     h->n_modes = n_modes;
     h->modes_stance = (int32_t)count_stance(modes, (size_t)n_modes);
+    WBC_HIP(plan_mode_loop(h, modes, n_modes));
     return WBC_OK;
 }
 
@@ -594,6 +659,15 @@ int32_t wbc_step_modes(wbc_engine* h, uint32_t flags) {
         au.batch = h->batch / h->n_modes;
         WBC_HIP(wbc_launch_update(&au, h->stream));
         WBC_HIP(launch_solves(h, a));
+    } else if (h->mode_loop > 1) {
+        // default, many states: one update per state and wave, then mode_loop hypotheses in turn
+        a.elim = 1;
+        h->elim = false;
+        a.mloop = h->mode_loop;
+        std::memcpy(a.mode_order, h->mode_order, sizeof(a.mode_order));
+        const int64_t S = h->batch / h->n_modes;
+        a.nwaves = (int32_t)(((S + wbc::QMAP_SEG - 1) / wbc::QMAP_SEG) * (h->n_modes / h->mode_loop));
+        WBC_HIP(wbc_launch_modes(&a, h->stream));
     } else {
         // default: each hypothesis reduced and solved in its own 16-lane segment
         WBC_HIP(begin_step16(h, a, flags));

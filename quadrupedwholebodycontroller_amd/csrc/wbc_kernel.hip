@@ -885,12 +885,12 @@ __device__ bool stance_reduce([[maybe_unused]] const KernelArgs& ka, [[maybe_unu
     ok = !seg_any<16>(!ok);  // every leg and S usable (uniform over the robot)
     lds_sync();
     // Y row i = W_i S^-1, q0_i = w_i + Y_i z
-    double yi[6];
+    double yi[6], q = 0.0;  // row i of Y and q0_i, kept for the Nt stage's DPP broadcasts
     {
         double wrow[6];
 #pragma unroll
         for (int c = 0; c < 6; ++c) wrow[c] = R.W[i][c];
-        double q = R.w[i];
+        q = R.w[i];
 #pragma unroll
         for (int c = 0; c < 6; ++c) {
             double a4[2] = {0.0, 0.0};
@@ -1000,23 +1000,27 @@ __device__ bool stance_reduce([[maybe_unused]] const KernelArgs& ka, [[maybe_unu
         gsv = -(((k == 0) ? wv[0] : (k == 1) ? wv[1] : wv[2]) - ((k == 0) ? cw[0] : (k == 1) ? cw[1] : cw[2]));
     }
     UST(ka, rb, 13);  // Y, H_f row, g_f
-    // Nt row j = (Mbj Y)_j Mb^-1 E^T + Jbj column j; t0_j = bbj_j + Mbj row j . q0
+    // Nt row j = (Mbj Y)_j Mb^-1 E^T + Jbj column j; t0_j = bbj_j + Mbj row j . q0.  Row kk of Y and
+    // q0_kk come from lane kk's registers by DPP (from LDS they were ~40 address adds, 40 reads and
+    // their waits), and each of the six sums runs as two chains of six
     const int j = i;
     {
-        double my[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, t4[2] = {0.0, 0.0}, s2 = 0.0;
+        double my[2][6] = {{0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0, 0.0, 0.0}}, t4[2] = {0.0, 0.0}, s2 = 0.0;
 #pragma unroll
         for (int kk = 0; kk < 12; ++kk) {
             const double mk = P.Mbj[j * 12 + kk], jc = P.Jbj[kk * 12 + j];
 #pragma unroll
-            for (int c = 0; c < 6; ++c) my[c] = fma(mk, R.Y[kk][c], my[c]);
-            t4[kk & 1] = fma(mk, R.q0[kk], t4[kk & 1]);
+            for (int c = 0; c < 6; ++c) my[kk & 1][c] = fma(mk, seg_bcast<16>(yi[c], kk), my[kk & 1][c]);
+            t4[kk & 1] = fma(mk, seg_bcast<16>(q, kk), t4[kk & 1]);
             s2 = fma(mk, mk, fma(jc, jc, s2));
         }
-        double mm[6];
+        double mm[6], ms[6];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) mm[c] = my[c] * inv_m;
+        for (int c = 0; c < 6; ++c) ms[c] = my[0][c] + my[1][c];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) mm[3 + c] = P.Icinv[3 * c] * my[3] + P.Icinv[3 * c + 1] * my[4] + P.Icinv[3 * c + 2] * my[5];
+        for (int c = 0; c < 3; ++c) mm[c] = ms[c] * inv_m;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) mm[3 + c] = P.Icinv[3 * c] * ms[3] + P.Icinv[3 * c + 1] * ms[4] + P.Icinv[3 * c + 2] * ms[5];
         double nt[12];
 #pragma unroll
         for (int lj = 0; lj < 4; ++lj) {
@@ -1034,7 +1038,7 @@ __device__ bool stance_reduce([[maybe_unused]] const KernelArgs& ka, [[maybe_unu
                     V.Nt[j * NTS_ST + c] = nt[c], V.Nt[j * NTS_ST + c + 1] = nt[c + 1];
 #pragma unroll
                 for (int c = 0; c < 6; c += 2) *reinterpret_cast<double2*>(&V.Y[j * 6 + c]) = make_double2(yi[c], yi[c + 1]);
-                V.q0[j] = R.q0[j];
+                V.q0[j] = q;
                 V.t0[j] = P.bbj[j] + (t4[0] + t4[1]);
                 V.nsel[j] = s2;
             }
@@ -1044,7 +1048,7 @@ __device__ bool stance_reduce([[maybe_unused]] const KernelArgs& ka, [[maybe_unu
                 *reinterpret_cast<double2*>(&pre->Nt[j * 12 + c]) = make_double2(nt[c], nt[c + 1]);
 #pragma unroll
             for (int c = 0; c < 6; c += 2) *reinterpret_cast<double2*>(&pre->Y[j * 6 + c]) = make_double2(yi[c], yi[c + 1]);
-            pre->q0[j] = R.q0[j];
+            pre->q0[j] = q;
             pre->t0[j] = P.bbj[j] + (t4[0] + t4[1]);
             pre->nsel[j] = s2;
         }
@@ -1070,7 +1074,7 @@ __device__ __forceinline__ void pk3(int k, const double* v, double* o) {  // row
     o[1] = (k == 0) ? v[2] : (k == 1) ? 0.0 : -v[0];
     o[2] = (k == 0) ? -v[1] : (k == 1) ? v[0] : 0.0;
 }
-__device__ bool rank6_factor(const Prob& P, UpdScratch& s, double gsv, int lane) {
+__device__ __forceinline__ bool rank6_factor(const Prob& P, UpdScratch& s, double gsv, int lane) {
     const int i = lane < 12 ? lane : 11, li = i / 3, ki = i % 3;
     double Hh[6][6];
 #pragma unroll
@@ -2155,10 +2159,25 @@ __device__ __forceinline__ void load_inputs(const KernelArgs& a, int rb, int lan
     }
 }
 
-template <int SUB, bool SOLVE = false, typename Model = wbc_model>
+// Leg row i's two bounds under its contact flags (cpp:384-402 finite differences, 447-464 swing
+// command): kr1 / ksw the row's R1 and swing masks (1 stance), ko the previous cycle's flag; one
+// definition for the update and the mode loop, so both round alike
+__device__ __forceinline__ void leg_bounds(double kr1, double ksw, double ko, double cur, double old, double cmd0,
+                                           double rdt, bool switching, double& r1, double& rsw) {
+    double jc_dot = 0.0, js_dot = 0.0;
+    if (!switching) {
+        jc_dot = (kr1 * cur - ko * old) * rdt;
+        js_dot = ((1.0 - ksw) * cur - (1.0 - ko) * old) * rdt;
+    }
+    const double cmd = cmd0 * (1.0 - ksw);
+    r1 = -jc_dot;
+    rsw = cmd - js_dot;
+}
+
+template <int SUB, bool SOLVE = false, typename Model = wbc_model, bool MLOOP = false>
 __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int lane, bool wr, UpdScratch& s, Prob& P,
                              Presolve* pre, const Model& md, const double* fric = nullptr,
-                             const double* vin = nullptr) {
+                             const double* vin = nullptr, int chunk = 0, unsigned* fails = nullptr) {
     const wbc_params& pr = a.pv;
     const bool switching = a.switching[rb] != 0;
     const bool stateful = a.stateful != 0;
@@ -2724,7 +2743,9 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
         }
     }
     UST(a, rb, 9);
-    // finite-difference bounds (cpp:384-402, 503-515); swing commands (cpp:447-464)
+    // finite-difference bounds (cpp:384-402, 503-515); swing commands (cpp:447-464).  Leg row i's
+    // terms stay in lane i for the mode loop, which re-masks them per hypothesis
+    double lb_cur = 0.0, lb_old = 0.0, lb_ko = 1.0, lb_cmd = 0.0;
     if (lane < 12) {
         const int i = lane, l = i / 3, rr = i % 3;
         const double d[3] = {P.d[3 * l], P.d[3 * l + 1], P.d[3 * l + 2]};
@@ -2749,15 +2770,9 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
         const double kn = (kap >> l) & 1, ko = (kap_old >> l) & 1;
         const bool unmasked = a.modes && !SOLVE;  // the split update of mode hypotheses
         const double kr1 = unmasked ? 1.0 : kn, ksw = unmasked ? 0.0 : kn;
-        double jc_dot = 0.0, js_dot = 0.0;
-        if (!switching) {
-            jc_dot = (kr1 * cur - ko * old) * rdt;
-            js_dot = ((1.0 - ksw) * cur - (1.0 - ko) * old) * rdt;
-        }
-        const double cmd = (ref[42 + i] + pr.kd_swing * (ref[30 + i] - s.vf[l][rr]) + pr.kp_swing * (ref[18 + i] - s.pf[l][rr])) *
-                           (1.0 - ksw);
-        P.r1[i] = -jc_dot;
-        P.rsw[i] = cmd - js_dot;
+        const double cmd0 = ref[42 + i] + pr.kd_swing * (ref[30 + i] - s.vf[l][rr]) + pr.kp_swing * (ref[18 + i] - s.pf[l][rr]);
+        leg_bounds(kr1, ksw, ko, cur, old, cmd0, rdt, switching, P.r1[i], P.rsw[i]);
+        lb_cur = cur; lb_old = old; lb_ko = ko; lb_cmd = cmd0;
     }
     // desired wrench (cpp:426-445); integralError_ update after use (cpp:442)
     if (lane < 6) {
@@ -2877,7 +2892,87 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
     // masks differ per QP: the stance elimination is formed for every state (the bounds are
     // written unmasked, i.e. as for stance legs, which is exactly the kappa = 15 hypothesis) and
     // the other hypotheses factor their slot Hessian in the solve.
-    if constexpr (SOLVE) {
+    if constexpr (SOLVE && MLOOP) {
+        // mode hypotheses, a.mloop of them per wave (wbc_modes_kernel): the state's update above once,
+        // then each hypothesis of the wave's chunk reduced and solved in turn, as the per-QP step
+        // below does it.  The reductions overwrite the update's P.Jbj (the general form's torque
+        // map) and Jf | A | KA (the stance form's Nt, the exchange column): 288 doubles, copied out
+        // once (to L2; in registers they spilled) and restored before each later hypothesis.  Everything else they read
+        // (the rest of P, the friction table) they leave alone.  A hypothesis whose reduction is not
+        // usable writes its problem to work row qp and sets bit it of *fails (the caller drains them)
+        static_assert(SUB == 16, "the inline solve runs in 16-lane segments");
+        const int K = a.modes, M = a.mloop;
+        double* flat = &s.Jf[0][0];
+        static_assert(offsetof(UpdScratch, A) == offsetof(UpdScratch, Jf) + sizeof(UpdScratch::Jf) &&
+                      offsetof(UpdScratch, KA) == offsetof(UpdScratch, A) + sizeof(UpdScratch::A) &&
+                      sizeof(UpdScratch::Jf) + sizeof(UpdScratch::A) + sizeof(UpdScratch::KA) == 144 * sizeof(double),
+                      "Jf | A | KA: one 144-double block");
+        // the copy: 2 x 144 doubles per segment in HBM (L2-resident), KernelArgs::mlbak row 4 w + seg
+        double* bak = a.mlbak + ((size_t)blockIdx.x * 4 + (threadIdx.x >> 4)) * 288;
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+            bak[lane + 16 * j] = P.Jbj[lane + 16 * j];
+            bak[144 + lane + 16 * j] = flat[lane + 16 * j];
+        }
+        unsigned fl = 0;
+        for (int it = 0; it < M; ++it) {
+            const int k = a.mode_order[chunk * M + it];
+            const int km = a.mode_masks[k] & 15;
+            // the lane and row laundered per hypothesis: left loop-invariant, every address and
+            // constant the reductions derive from them was hoisted out of the loop and held across it
+            // (~180 spill instructions)
+            int ln = lane, rw = rb;
+            asm volatile("" : "+v"(ln), "+v"(rw));
+            const int lane = ln, rb = rw;
+            const int q = rb * K + k;
+            lds_sync();  // the previous hypothesis is done with the problem and the scratch
+            if (it > 0) {
+                double kj[9], ks[9];
+#pragma unroll
+                for (int j = 0; j < 9; ++j) {
+                    kj[j] = bak[lane + 16 * j];
+                    ks[j] = bak[144 + lane + 16 * j];
+                }
+#pragma unroll
+                for (int j = 0; j < 9; ++j) {
+                    P.Jbj[lane + 16 * j] = kj[j];
+                    flat[lane + 16 * j] = ks[j];
+                }
+            }
+            if (lane < 12) {
+                const double kn = (km >> (lane / 3)) & 1;
+                leg_bounds(kn, kn, lb_ko, lb_cur, lb_old, lb_cmd, rdt, switching, P.r1[lane], P.rsw[lane]);
+            }
+            if (lane == 0) P.kappa = (double)km;
+            lds_sync();
+            bool ok;
+            if (km == 15) {  // stateless mask 15: the four-contact stance form
+                double hrow[12], gsv = 0.0;
+                ok = stance_reduce<true>(a, rb, P, pr, lane, wr, s, hrow, gsv, nullptr) && rank6_factor(P, s, gsv, lane);
+                if (ok) solve16<true, false>(a, rb, q, lane, wr, P, s, St16(s, fric), 15, WBC_QP_OK);
+            } else {
+                const St16 V(s, P, fric);
+                bool vac = false;
+                ok = reduce_general(a, rb, P, pr, lane, km, s, V, vac);
+                if (ok) solve16<true, true>(a, rb, q, lane, wr, P, s, V, km, vac ? WBC_QP_INFEASIBLE : WBC_QP_OK);
+            }
+            if (!ok && wr) {  // as wbc_update_solve_kernel's fallback record
+                lds_sync();
+                const double2* src = reinterpret_cast<const double2*>(&P);
+                double* wrow = a.work + (size_t)q * WORK_LEN;
+                double2* dst = reinterpret_cast<double2*>(wrow);
+                for (int e = lane; e < PROB_LEN / 2; e += SUB) dst[e] = src[e];
+                if (lane == 0) {
+                    Presolve* pw = reinterpret_cast<Presolve*>(wrow + PROB_LEN);
+                    pw->presolved = 0.0;
+                    pw->stance = 0.0;
+                }
+                fl |= 1u << it;
+            }
+        }
+        *fails = fl;
+        return true;
+    } else if constexpr (SOLVE) {
         static_assert(SUB == 16, "the inline solve runs in 16-lane segments");
         // a stateless QP of mask 15: the four-contact stance form (stance_reduce + the rank-6
         // factor, no Hessian to factor); every other QP: the general form (its own mask, a hotstart
@@ -4253,6 +4348,9 @@ static_assert(sizeof(SolveLds) <= sizeof(UpdLds), "the drain reuses the update s
 // A call (the rare path stays out of the kernel's register allocation), handed the address of the
 // kernel's arguments in its kernarg segment (passing the struct would pin a stack copy to the whole
 // kernel; a callee has no kernarg pointer of its own).
+// (One instance per calling kernel, TAG: a shared callee is allocated for the larger of its callers'
+// register budgets, which raised the default step's to 512 registers and its scratch to 2.2 KB.)
+template <int TAG>
 __device__ __attribute__((noinline)) void drain_fallbacks(const KernelArgs* ka, unsigned long long fm, int qp,
                                                           SolveLds* L) {
     KernelArgs f = *ka;
@@ -4339,8 +4437,38 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) {
     }
     const unsigned long long fm = __ballot(fb && lane == 0);
     if (fm)
-        drain_fallbacks((const KernelArgs*)__builtin_amdgcn_kernarg_segment_ptr(), fm, qp,
-                        reinterpret_cast<SolveLds*>(&L));
+        drain_fallbacks<0>((const KernelArgs*)__builtin_amdgcn_kernarg_segment_ptr(), fm, qp,
+                           reinterpret_cast<SolveLds*>(&L));
+}
+
+// Mode hypotheses with the update shared (KernelArgs::mloop = M > 1): workgroup g C + c (C = K / M
+// chunks, xcd_block order, so a state group's chunks share an L2) runs states 4 g .. 4 g + 3, each
+// segment through one update and then the M hypotheses of chunk c (update_phase's mode loop);
+// the update's share of a hypothesis falls from one whole update to 1 / M of one.  Outputs,
+// fallbacks and their records are the per-hypothesis step's.
+WBC_UPDATE_KERNEL_ATTR void wbc_modes_kernel(KernelArgs a) {
+    __shared__ UpdLds L;
+    const int seg = (int)threadIdx.x / UPD_SUB, lane = (int)threadIdx.x % UPD_SUB;
+    const int K = a.modes, M = a.mloop, C = K / M;
+    const int blk = xcd_block((int)blockIdx.x, (int)gridDim.x);
+    const int S = a.batch / K, g = blk / C, c = blk - g * C;
+    int row = 4 * g + seg;
+    const bool wr = row < S;  // a padding segment recomputes the last state, writes nothing
+    if (!wr) row = S - 1;
+    const int k0 = a.mode_order[c * M];
+    double vin[(91 + UPD_SUB - 1) / UPD_SUB];
+    load_inputs<UPD_SUB>(a, row, lane, vin);
+    stage_to_lds<LIMG_LEN>(reinterpret_cast<double*>(&L), a.limg, (int)threadIdx.x);
+    lds_sync();
+    unsigned fails = 0;
+    update_phase<UPD_SUB, true, LdsModel, true>(a, row, row * K + k0, a.mode_masks[k0] & 15, lane, wr, L.u[seg],
+                                                L.prob[seg], nullptr, L.model, &L.fric[0], vin, c, &fails);
+    for (int it = 0; it < M; ++it) {
+        const unsigned long long fm = __ballot(wr && lane == 0 && ((fails >> it) & 1u));
+        if (fm)
+            drain_fallbacks<1>((const KernelArgs*)__builtin_amdgcn_kernarg_segment_ptr(), fm,
+                               row * K + a.mode_order[c * M + it], reinterpret_cast<SolveLds*>(&L));
+    }
 }
 
 // Four-contact QP whose equalities the update kernel eliminated (its Presolve::stance flag, in
@@ -4523,6 +4651,11 @@ extern "C" hipError_t wbc_launch_solve_stance(const wbc::KernelArgs* a, hipStrea
 // The default step in one launch: the update kernel reducing and solving every QP inline, and the
 // QPs whose reduction was not usable with the general method in the same wave (drain_fallbacks:
 // their records carry their own mask and bounds, so the general solve runs them with modes = 0).
+extern "C" hipError_t wbc_launch_modes(const wbc::KernelArgs* a, hipStream_t st) {
+    if (a->nwaves <= 0 || a->modes <= 0 || a->mloop <= 0 || a->modes % a->mloop != 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(wbc::wbc_modes_kernel, dim3(a->nwaves), dim3(64), 0, st, *a);
+    return hipGetLastError();
+}
 extern "C" hipError_t wbc_launch_update_solve(const wbc::KernelArgs* a, hipStream_t st) {
     static_assert(wbc::UPD_RPW == wbc::QMAP_SEG, "the wave map's segments are the kernel's");
     if (a->nwaves <= 0) return hipErrorInvalidValue;

@@ -163,6 +163,13 @@ struct KernelArgs {
     // mask modes[k]) and qmap is unused.  nwaves: the step kernel's grid.
     const int32_t* qmap;
     int32_t nwaves;
+    // Mode hypotheses with the state's update shared (wbc_modes_kernel): each wave holds four
+    // states and a chunk of mloop hypotheses, solved one after another after one update; chunk c
+    // runs hypotheses mode_order[c mloop .. c mloop + mloop - 1].  mloop = 0: one hypothesis per
+    // segment (wbc_update_solve_kernel's arithmetic map).
+    int32_t mloop;
+    uint8_t mode_order[16];
+    double* mlbak;  // [nwaves * 4][288]: each segment's copy of the reduction inputs the reductions overwrite
     // the parameters by value: read from the kernel-argument segment (scalar loads of memory the
     // compiler knows is constant), not through `params`, whose global loads it must repeat after
     // every global store and wait for in turn

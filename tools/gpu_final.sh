@@ -27,6 +27,7 @@ done
 step b1_fused 120 quadrupedwholebodycontroller_amd/wbc_control_loop stance 3000 0 fused
 step b1_default 120 quadrupedwholebodycontroller_amd/wbc_control_loop stance 3000 0 default
 step b1_probe 120 python tools/b1_probe.py 2000
+step batch_sweep 180 python tools/batch_sweep.py 50
 step ust_stance 120 env WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_istamps.so python tools/ust16.py stance_cold 4096
 step ust_rl 120 env WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_istamps.so python tools/ust16.py rl_random 8192
 tail -1 $O/bench.log
