@@ -3,8 +3,8 @@
 
 One step = one wbc_step over the rank's batch (dynamics + centroidal assembly + QP + torques: one
 kernel, wbc_update_solve_kernel, four QPs per wave, each reduced exactly to 12 variables and
-solved in place; a QP whose reduction is not usable is solved by the same wave's general method),
-plus for N > 1 the RCCL all-gather of the torque block.  Inputs are
+solved in place; a QP whose reduction is not usable is solved by the same wave's general method;
+mode hypotheses with many states: wbc_modes_kernel, one update per state and wave), plus for N > 1 the RCCL all-gather of the torque block.  Inputs are
 resident in HBM before the timed region.  Default workload: configs[1] of BASELINE.json,
 B = 4096 four-contact stance states, cold solves, per GPU (weak scaling).
 
@@ -41,8 +41,8 @@ CONFIGS = {
                             desc="BASELINE configs[3] per-GPU shard: randomized q/qd, 16 contact masks, cold"),
     "modes16_b16384": dict(gen="modes16", batch=16384, seed=4, modes=16, scaling="weak",
                            desc="BASELINE configs[4] per-GPU shard: 1024 states x all 16 contact masks, cold; "
-                                "wbc_step_modes (one 16-lane segment per hypothesis, the state's inputs shared "
-                                "through L2)"),
+                                "wbc_step_modes (the mode loop: one update per state and wave, then four "
+                                "hypotheses in turn, wbc_modes_kernel)"),
     # the two multi-GPU configurations at their global sizes (strong scaling: total work fixed)
     "rl_random_b65536": dict(gen="rl_random", batch=65536, seed=3, scaling="strong",
                              desc="BASELINE configs[3]: global B=65536 randomized q/qd (16 contact masks, cold), "
@@ -178,11 +178,17 @@ def step_flops(S, iters):
     return float(S * (F_DYN + F_ASM) + np.sum(F_FACT + F_TAU + F_ITER * iters))
 
 
-def roofline_of(flops, kernel_ms, traffic=None, traffic_src=None):
+def step_kernel(e):
+    """The one kernel of the engine's default step: wbc_modes_kernel under the mode loop (mode
+    hypotheses, many states), wbc_update_solve_kernel otherwise."""
+    return "wbc_modes_kernel" if e.modes_per_wave() > 1 else "wbc_update_solve_kernel"
+
+
+def roofline_of(flops, kernel_ms, traffic=None, traffic_src=None, kernel="wbc_update_solve_kernel"):
     tf = flops / (kernel_ms * 1e-3) / 1e12
     return {"bound": "fp64_valu", "achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": tf / FP64_PEAK_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
-            "kernel": "wbc_update_solve_kernel", "kernel_ms": kernel_ms, "flops_per_launch": flops}
+            "kernel": kernel, "kernel_ms": kernel_ms, "flops_per_launch": flops}
 
 
 def make_engine(cfg, B, seed, device, stream):
@@ -427,15 +433,16 @@ def main():
         torch.cuda.synchronize()
         return ev0.elapsed_time(ev1) / args.steps
 
-    # A step is one kernel (wbc_update_solve_kernel: dynamics, the QP reduced to 12 variables and
-    # solved in the same wave, torques; the rare unusable reduction solved there too by the general
-    # method): the step's time is that kernel's.  It owns all of SURVEY 8(d)'s flops.
+    # A step is one kernel (wbc_update_solve_kernel, or wbc_modes_kernel for mode hypotheses under
+    # the mode loop: dynamics, the QP reduced to 12 variables and solved in the same wave, torques;
+    # the rare unusable reduction solved there too by the general method): the step's time is that
+    # kernel's.  It owns all of SURVEY 8(d)'s flops.
     step_ms = timed(lambda: step(STEP_FLAGS))
     out = e.outputs()
     iters = out["iters"].astype(np.int64)
     status = out["status"]
-    kernels = {"wbc_update_solve_kernel": step_ms}
-    dom, dom_ms = "wbc_update_solve_kernel", step_ms
+    dom, dom_ms = step_kernel(e), step_ms
+    kernels = {dom: step_ms}
     flops_step = step_flops(S, iters)
     tf_dom = flops_step / (dom_ms * 1e-3) / 1e12
     bytes_step = S * BYTES_IN + B * BYTES_OUT
@@ -463,7 +470,8 @@ def main():
             extra[name] = dict(batch=B2, ms_per_step=ms2, solves_per_s=B2 / (ms2 * 1e-3),
                                status_counts=np.bincount(o2["status"], minlength=4).tolist(),
                                mean_iters=float(o2["iters"].mean()), desc=c2["desc"],
-                               roofline=roofline_of(step_flops(S2, o2["iters"]), ms2, tr2.get("step"), tr2_src),
+                               roofline=roofline_of(step_flops(S2, o2["iters"]), ms2, tr2.get("step"), tr2_src,
+                                                    step_kernel(e2)),
                                traffic_per_step=tr2.get("step"), traffic_source=tr2_src,
                                algorithmic_bytes_per_step=float(S2 * BYTES_IN + B2 * BYTES_OUT))
             e2.close()
@@ -493,7 +501,7 @@ def main():
                      "frac": tf_dom / FP64_PEAK_TFLOPS, "traffic": traffic.get(dom),
                      "traffic_source": traffic_src, "kernel": dom, "kernel_ms": dom_ms,
                      "kernels_ms": kernels, "step_kernels_ms": step_ms,
-                     "note": "the step's one kernel (wbc_update_solve_kernel; its kernel_ms is the step's, HIP events "
+                     "note": f"the step's one kernel ({dom}; its kernel_ms is the step's, HIP events "
                              "around back-to-back launches); fp64 VALU roof (no MFMA on this path; gfx950 fp64 "
                              "vector peak); SURVEY 8(d) algorithmic flops: F_dyn + F_asm per state, F_fact + F_tau + "
                              "k F_iter per QP, k = iters[] (working-set changes of the 12-variable form the engine "

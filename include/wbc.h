@@ -222,6 +222,12 @@ int32_t wbc_synchronize(wbc_engine* h);
 #define WBC_MAX_MODES 16
 int32_t wbc_set_modes(wbc_engine* h, int32_t n_modes, const uint8_t* modes);
 int32_t wbc_step_modes(wbc_engine* h, uint32_t flags);
+/* Hypotheses per wave of the default wbc_step_modes (no reference counterpart; diagnostics): 1 =
+ * one hypothesis per 16-lane segment (wbc_update_solve_kernel); M > 1 = the mode loop
+ * (wbc_modes_kernel: one update per state and wave, then M hypotheses in turn), chosen by
+ * wbc_set_modes from the batch and the device's CU count (WBC_MODES_M in the environment overrides
+ * it with a divisor of n_modes).  Results are bit-identical either way. */
+int32_t wbc_modes_per_wave(wbc_engine* h, int32_t* m);
 
 /* One synchronous control cycle, host arrays in and out (the low-latency path for small batches,
  * e.g. the B = 1 drop-in of whole_body_controller_node): the inputs are packed into pinned staging

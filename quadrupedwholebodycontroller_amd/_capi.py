@@ -26,7 +26,7 @@ DBG = dict(COM=0, COMVEL=3, POSE=6, VC=12, M=18, CNU=342, JFEET=360, PFEET=576, 
 C_API_SYMBOLS = [
     "wbc_default_params", "wbc_anymal_model", "wbc_create", "wbc_destroy", "wbc_batch", "wbc_set_stream",
     "wbc_set_state", "wbc_set_reference", "wbc_bind_device_inputs", "wbc_bind_device_outputs", "wbc_reset", "wbc_update", "wbc_solve",
-    "wbc_step", "wbc_set_modes", "wbc_step_modes", "wbc_cycle", "wbc_synchronize", "wbc_get_output", "wbc_device_outputs", "wbc_get_debug", "wbc_last_kernel_ms",
+    "wbc_step", "wbc_set_modes", "wbc_step_modes", "wbc_modes_per_wave", "wbc_cycle", "wbc_synchronize", "wbc_get_output", "wbc_device_outputs", "wbc_get_debug", "wbc_last_kernel_ms",
     "wbc_last_error", "wbc_model_from_urdf",
 ]
 
@@ -88,6 +88,7 @@ def load_library(path: str = LIB_PATH):
         "wbc_set_modes": ([P, I32, P], I32),
         "wbc_cycle": ([P, P, P, P, P, P, P, U32, P, P, P, P, P], I32),
         "wbc_step_modes": ([P, U32], I32),
+        "wbc_modes_per_wave": ([P, C.POINTER(C.c_int32)], I32),
         "wbc_synchronize": ([P], I32),
         "wbc_get_output": ([P, P, P, P, P, P], I32),
         "wbc_device_outputs": ([P, C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(P)], I32),
@@ -246,6 +247,13 @@ class Engine:
     def step_modes(self, flags: int = 1):
         """wbc_step_modes: one cold step of every (state, mode) hypothesis (flags need STATELESS)."""
         self._check(self.lib.wbc_step_modes(self.h, flags), "wbc_step_modes")
+
+    def modes_per_wave(self) -> int:
+        """wbc_modes_per_wave: hypotheses per wave of wbc_step_modes (1: one per segment; M > 1: the
+        mode loop, wbc_modes_kernel); 0 without modes."""
+        m = C.c_int32(0)
+        self._check(self.lib.wbc_modes_per_wave(self.h, C.byref(m)), "wbc_modes_per_wave")
+        return int(m.value)
 
     def synchronize(self):
         self._check(self.lib.wbc_synchronize(self.h), "wbc_synchronize")

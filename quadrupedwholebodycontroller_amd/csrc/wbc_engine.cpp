@@ -67,8 +67,6 @@ struct wbc_engine {
     // and the hypotheses' order, chunk by chunk (plan_mode_loop)
     int32_t mode_loop = 1;
     uint8_t mode_order[16] = {};
-    double* d_mlbak = nullptr;  // KernelArgs::mlbak, sized for the mode loop's grid
-    size_t mlbak_len = 0;
     // bound (possibly external) inputs
     const double* in_pose = nullptr;
     const double* in_nu = nullptr;
@@ -177,7 +175,6 @@ wbc::KernelArgs make_args(wbc_engine* h, uint32_t flags) {
     a.nwaves = (h->batch + wbc::QMAP_SEG - 1) / wbc::QMAP_SEG;
     a.mloop = 0;
     std::memset(a.mode_order, 0, sizeof(a.mode_order));
-    a.mlbak = h->d_mlbak;
     return a;
 }
 
@@ -204,7 +201,7 @@ hipError_t drain(wbc_engine* h) { return h->stream ? hipStreamSynchronize(h->str
 // estimated work so far (LPT), so the chunks' waves end together: the estimate is a reduction and
 // solve of 30 units plus 3 per expected working-set pass (0.3, 2.3, 4.5, 6.7, 8.9
 // passes for 0 .. 4 stance legs).
-hipError_t plan_mode_loop(wbc_engine* h, const uint8_t* modes, int32_t K) {
+void plan_mode_loop(wbc_engine* h, const uint8_t* modes, int32_t K) {
     const int64_t groups = (h->batch / K + 3) / 4;
     int cus = 256;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || cus <= 0) cus = 256;
@@ -233,20 +230,6 @@ hipError_t plan_mode_loop(wbc_engine* h, const uint8_t* modes, int32_t K) {
     for (int c = 0; c < C; ++c)
         for (int i = 0; i < M; ++i) h->mode_order[c * M + i] = chunk[c][i];
     h->mode_loop = M;
-    // each segment's copy of the reduction inputs (KernelArgs::mlbak); the stream is idle here
-    const size_t need = M > 1 ? (size_t)groups * C * 4 * 288 : 0;
-    if (need > h->mlbak_len) {
-        if (h->d_mlbak) (void)hipFree(h->d_mlbak);
-        h->d_mlbak = nullptr;
-        h->mlbak_len = 0;
-        hipError_t e = hipMalloc(reinterpret_cast<void**>(&h->d_mlbak), need * sizeof(double));
-        if (e != hipSuccess) {
-            h->mode_loop = 1;  // the per-hypothesis step needs no copy
-            return e;
-        }
-        h->mlbak_len = need;
-    }
-    return hipSuccess;
 }
 
 int64_t count_stance(const uint8_t* masks, size_t n) {
@@ -470,7 +453,7 @@ int32_t wbc_destroy(wbc_engine* h) {
     // which would also wait for other engines' and the caller's unrelated work)
     (void)drain(h);
     void* ptrs[] = {h->d_model, h->d_params, h->d_limg, h->d_inblk, h->d_outblk, h->d_mask, h->d_modes, h->d_hist, h->d_work,
-                    h->d_fb, h->d_dbg, h->d_qmap, h->d_mlbak};
+                    h->d_fb, h->d_dbg, h->d_qmap};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (h->h_in) (void)hipHostFree(h->h_in);
@@ -636,7 +619,7 @@ int32_t wbc_set_modes(wbc_engine* h, int32_t n_modes, const uint8_t* modes) {
     WBC_HIP(hipStreamSynchronize(h->stream));
     h->n_modes = n_modes;
     h->modes_stance = (int32_t)count_stance(modes, (size_t)n_modes);
-    WBC_HIP(plan_mode_loop(h, modes, n_modes));
+    plan_mode_loop(h, modes, n_modes);
     return WBC_OK;
 }
 
@@ -835,6 +818,12 @@ int32_t wbc_get_debug(wbc_engine* h, double* out) {
     WBC_HIP(hipSetDevice(h->device));
     WBC_HIP(hipMemcpyAsync(out, h->d_dbg, (size_t)h->batch * WBC_DBG_LEN * sizeof(double), hipMemcpyDeviceToHost, h->stream));
     WBC_HIP(hipStreamSynchronize(h->stream));
+    return WBC_OK;
+}
+
+int32_t wbc_modes_per_wave(wbc_engine* h, int32_t* m) {
+    if (!h || !m) return fail(WBC_ERR_ARG, "null handle or output");
+    *m = h->n_modes ? h->mode_loop : 0;
     return WBC_OK;
 }
 

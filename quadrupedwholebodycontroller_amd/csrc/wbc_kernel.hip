@@ -2896,8 +2896,9 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
         // mode hypotheses, a.mloop of them per wave (wbc_modes_kernel): the state's update above once,
         // then each hypothesis of the wave's chunk reduced and solved in turn, as the per-QP step
         // below does it.  The reductions overwrite the update's P.Jbj (the general form's torque
-        // map) and Jf | A | KA (the stance form's Nt, the exchange column): 288 doubles, copied out
-        // once (to L2; in registers they spilled) and restored before each later hypothesis.  Everything else they read
+        // map) and Jf | A | KA (the stance form's Nt, the exchange column): 288 doubles, 18 per lane,
+        // kept in registers and restored before each later hypothesis (a copy through L2 instead
+        // was 9.4 MB written per step at configs[4]'s shard).  Everything else they read
         // (the rest of P, the friction table) they leave alone.  A hypothesis whose reduction is not
         // usable writes its problem to work row qp and sets bit it of *fails (the caller drains them)
         static_assert(SUB == 16, "the inline solve runs in 16-lane segments");
@@ -2907,12 +2908,11 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
                       offsetof(UpdScratch, KA) == offsetof(UpdScratch, A) + sizeof(UpdScratch::A) &&
                       sizeof(UpdScratch::Jf) + sizeof(UpdScratch::A) + sizeof(UpdScratch::KA) == 144 * sizeof(double),
                       "Jf | A | KA: one 144-double block");
-        // the copy: 2 x 144 doubles per segment in HBM (L2-resident), KernelArgs::mlbak row 4 w + seg
-        double* bak = a.mlbak + ((size_t)blockIdx.x * 4 + (threadIdx.x >> 4)) * 288;
+        double kj[9], ks[9];
 #pragma unroll
         for (int j = 0; j < 9; ++j) {
-            bak[lane + 16 * j] = P.Jbj[lane + 16 * j];
-            bak[144 + lane + 16 * j] = flat[lane + 16 * j];
+            kj[j] = P.Jbj[lane + 16 * j];
+            ks[j] = flat[lane + 16 * j];
         }
         unsigned fl = 0;
         for (int it = 0; it < M; ++it) {
@@ -2927,12 +2927,6 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
             const int q = rb * K + k;
             lds_sync();  // the previous hypothesis is done with the problem and the scratch
             if (it > 0) {
-                double kj[9], ks[9];
-#pragma unroll
-                for (int j = 0; j < 9; ++j) {
-                    kj[j] = bak[lane + 16 * j];
-                    ks[j] = bak[144 + lane + 16 * j];
-                }
 #pragma unroll
                 for (int j = 0; j < 9; ++j) {
                     P.Jbj[lane + 16 * j] = kj[j];

@@ -169,7 +169,6 @@ struct KernelArgs {
     // segment (wbc_update_solve_kernel's arithmetic map).
     int32_t mloop;
     uint8_t mode_order[16];
-    double* mlbak;  // [nwaves * 4][288]: each segment's copy of the reduction inputs the reductions overwrite
     // the parameters by value: read from the kernel-argument segment (scalar loads of memory the
     // compiler knows is constant), not through `params`, whose global loads it must repeat after
     // every global store and wait for in turn

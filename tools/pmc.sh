@@ -10,8 +10,8 @@ BATCH=${BATCH:-4096}
 OUT=gpurun_out/pmc_$TAG
 mkdir -p $OUT
 CMD="python3 bench.py --config $CONFIG --steps 10 --warmup 2 --no-cpu-baseline"
-# every bench config's step is one kernel (the default step)
-STEPK=wbc_update_solve_kernel
+# every bench config's step is one kernel: the default step's, or the mode loop's for hypotheses
+STEPK=wbc_update_solve_kernel,wbc_modes_kernel
 i=0
 for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" \
            "SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU SQ_WAIT_INST_LDS" \

@@ -59,8 +59,11 @@ def main():
                             "+ WRITE_SIZE, KiB -> B; separate --pmc passes with --kernel-trace only; widths other "
                             "than 16 B/lane are uncalibrated (MI355X_MICROARCH.md)")}
     traffic = {k: traffic_bytes(m) for k, m in mean.items()}
-    if all(traffic.get(k) is not None for k in step_kernels):
-        traffic["step"] = sum(traffic[k] for k in step_kernels)
+    # the step's kernels that ran (the default step runs one of them: wbc_update_solve_kernel, or
+    # wbc_modes_kernel for mode hypotheses under the mode loop)
+    ran = [k for k in step_kernels if traffic.get(k) is not None]
+    if ran:
+        traffic["step"] = sum(traffic[k] for k in ran)
     rec["traffic"] = traffic
     rec["per_wave"] = {k: {c: v / m["SQ_WAVES"] for c, v in m.items() if c.startswith("SQ_INSTS")}
                        for k, m in mean.items() if m.get("SQ_WAVES")}

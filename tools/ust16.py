@@ -1,7 +1,8 @@
 """Cycles per stage of the default step kernel (wbc_update_solve_kernel: four QPs per wave, each
 reduced to 12 variables and solved in its 16-lane segment), from the WBC_ISTAMPS build: medians over
 waves (lane 0 of each wave writes the stamps, so only QPs qp % 4 == 0 carry them).
-Usage (GPU box): WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_istamps.so python tools/ust16.py [config] [B]"""
+Usage (GPU box): WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_istamps.so python tools/ust16.py [config] [B]
+(config: a stateless workloads generator, or trot: configs[2]'s stateful trot, its 60th cycle)"""
 import json, os, sys
 import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -9,12 +10,18 @@ from quadrupedwholebodycontroller_amd import STATELESS, Engine, workloads
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "stance_cold"
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
-inp = getattr(workloads, cfg)(B, seed=1 if cfg == "stance_cold" else 3)
 e = Engine(B)
-e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
-e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
-for _ in range(3):
-    e.step(STATELESS)
+if cfg == "trot":  # configs[2]: stateful (history, hotstart), the stamps of its 60th cycle
+    for k, s in enumerate(workloads.trot_sequence(B, steps=60, seed=2)):
+        e.set_state(s["base_pose"], s["nu"], s["qj"])
+        e.set_reference(s["ref"], s["contacts"], s["switching"])
+        e.step(0)
+else:
+    inp = getattr(workloads, cfg)(B, seed=1 if cfg == "stance_cold" else 3)
+    e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
+    e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
+    for _ in range(3):
+        e.step(STATELESS)
 e.synchronize()
 D = e.debug()[0::4]
 st = lambda i: D[:, 8 + i]  # UST(i)
