@@ -98,6 +98,8 @@ def load_library(path: str = LIB_PATH):
         "wbc_model_from_urdf": ([C.c_char_p, P, P, C.c_char_p, C.POINTER(WbcModel)], I32),
     }
     for name, (argt, rest) in sig.items():
+        if name == "wbc_modes_per_wave" and not hasattr(lib, name):
+            continue  # a diagnostic entry point: earlier builds (A/B variants, tools/build_rev.sh) lack it
         fn = getattr(lib, name)
         fn.argtypes = argt
         fn.restype = rest

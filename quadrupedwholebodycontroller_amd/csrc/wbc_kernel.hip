@@ -1657,7 +1657,9 @@ __device__ __forceinline__ int seg_shfl_i(int v, int j) {
 // GEN: the general form of any contact mask (reduce_general, St16(s, P)): friction rows only for
 // stance legs, the hotstart of stateful steps, the outputs mapped back through B, Y and the leg
 // rows; otherwise the four-contact stance form (stateless).  qp = output row, hr = history row.
-template <bool ROWS, bool GEN>
+// STF: -1 stateful or not by KernelArgs::stateful at run time; 0 / 1 known at compile time (the
+// default step's two instances, wbc_update_solve_kernel<STF>)
+template <bool ROWS, bool GEN, int STF = -1>
 __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, const Prob& P, UpdScratch& s,
                         const St16& V, int kap, int status0) {
     constexpr int N = 12;
@@ -1809,7 +1811,7 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
     // point where every warm row holds with equality: v = -R^-T s_A(x0), u = R^-1 v, x = x0 + J v.
     // A dependent warm row or a multiplier below -1e-10 rejects the set: cold start from x0.
     if constexpr (GEN) {
-        if (!done && a.stateful && !a.cold) {
+        if (!done && (STF < 0 ? a.stateful != 0 : STF == 1) && !a.cold) {
             const double* H = a.hist + (size_t)rb * HIST_LEN;
             const double tag = H[H_WSKAP];
             unsigned long long ws = (tag >= 16.0) ? ((unsigned long long)(unsigned)H[H_WSLO] |
@@ -2117,7 +2119,7 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
         a.status[qp] = status;
         a.iters[qp] = iters;
     }
-    if (GEN && a.stateful && wr) {  // working set for the next cycle's hotstart, this numbering
+    if (GEN && (STF < 0 ? a.stateful != 0 : STF == 1) && wr) {  // working set for the next cycle's hotstart, this numbering
         const unsigned long long b0 = __ballot((ab & 1) != 0), b1 = __ballot((ab & 2) != 0), b2 = __ballot((ab & 4) != 0);
         const int sh = (int)threadIdx.x & 48;
         const unsigned long long ws = ((b0 >> sh) & 0xFFFFull) | (((b1 >> sh) & 0xFFFFull) << 16) |
@@ -2174,13 +2176,13 @@ __device__ __forceinline__ void leg_bounds(double kr1, double ksw, double ko, do
     rsw = cmd - js_dot;
 }
 
-template <int SUB, bool SOLVE = false, typename Model = wbc_model, bool MLOOP = false>
+template <int SUB, bool SOLVE = false, typename Model = wbc_model, bool MLOOP = false, int STF = -1>
 __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int lane, bool wr, UpdScratch& s, Prob& P,
                              Presolve* pre, const Model& md, const double* fric = nullptr,
                              const double* vin = nullptr, int chunk = 0, unsigned* fails = nullptr) {
     const wbc_params& pr = a.pv;
     const bool switching = a.switching[rb] != 0;
-    const bool stateful = a.stateful != 0;
+    const bool stateful = STF < 0 ? a.stateful != 0 : STF == 1;  // (STF: as solve16's)
     const bool debug = a.debug != 0;
     double* H = stateful ? a.hist + (size_t)rb * HIST_LEN : nullptr;
     UST(a, rb, 0);
@@ -2241,6 +2243,35 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
     }
     lds_sync();
     UST(a, rb, 1);
+    // The old history this lane reads, loaded in one batch (addresses clamped, so every lane loads
+    // unconditionally).  Read where they are used, the loads sat in lane-dependent branches and
+    // after history stores the compiler cannot order them against, so it issued and waited for
+    // them group by group: about ten serialized memory round trips per stateful update.  The
+    // stateful instance of the default step (STF = 1) issues the batch here, so that its HBM round
+    // trip overlaps stages A-C; the others where the history is first used (after stage C).
+    constexpr int NT = (18 + SUB - 1) / SUB;  // Tdot_inv columns per lane
+    double hTd[18], hMa[NT][6], hR[3], hDo[3], hJo[12], hE = 0.0, hv = 0.0, hk = 15.0;
+    auto load_hist = [&]() {
+        const int l6 = lane < 6 ? lane : 5, l12 = lane < 12 ? lane : 11;
+        hv = H[H_VALID];
+        hk = H[H_KOLD];
+#pragma unroll
+        for (int cc = 0; cc < 18; ++cc) hTd[cc] = H[H_TDINV + l6 * 18 + cc];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) hR[i] = H[H_ROLD + i];
+#pragma unroll
+        for (int it = 0; it < NT; ++it) {
+            const int jj = lane + it * SUB - 6, j = jj < 0 ? 0 : (jj > 11 ? 11 : jj);
+#pragma unroll
+            for (int rr = 0; rr < 6; ++rr) hMa[it][rr] = H[H_MAOLD + rr * 12 + j];
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) hDo[k] = H[H_DOLD + 3 * (l12 / 3) + k];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) hJo[j] = H[H_JBJOLD + l12 * 12 + j];
+        hE = H[H_EINT + l6];
+    };
+    if constexpr (STF == 1) load_hist();
     const double* pB = &s.in[0];
     const double* vB = &s.in[7];
     const double* wB = &s.in[10];
@@ -2520,30 +2551,8 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
     double y[6] = {0, 0, 0, 0, 0, 0};
     bool hvalid = false;
     int kap_old = 15;
-    // The old history this lane reads, loaded in one batch (addresses clamped, so every lane loads
-    // unconditionally).  Read where they are used, the loads sit in lane-dependent branches and
-    // after history stores the compiler cannot order them against, so it issued and waited for
-    // them group by group: about ten serialized memory round trips per stateful update.
-    constexpr int NT = (18 + SUB - 1) / SUB;  // Tdot_inv columns per lane
-    double hTd[18], hMa[NT][6], hR[3], hDo[3], hJo[12], hE = 0.0;
     if (stateful) {
-        const int l6 = lane < 6 ? lane : 5, l12 = lane < 12 ? lane : 11;
-        const double hv = H[H_VALID], hk = H[H_KOLD];
-#pragma unroll
-        for (int cc = 0; cc < 18; ++cc) hTd[cc] = H[H_TDINV + l6 * 18 + cc];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) hR[i] = H[H_ROLD + i];
-#pragma unroll
-        for (int it = 0; it < NT; ++it) {
-            const int jj = lane + it * SUB - 6, j = jj < 0 ? 0 : (jj > 11 ? 11 : jj);
-#pragma unroll
-            for (int rr = 0; rr < 6; ++rr) hMa[it][rr] = H[H_MAOLD + rr * 12 + j];
-        }
-#pragma unroll
-        for (int k = 0; k < 3; ++k) hDo[k] = H[H_DOLD + 3 * (l12 / 3) + k];
-#pragma unroll
-        for (int j = 0; j < 12; ++j) hJo[j] = H[H_JBJOLD + l12 * 12 + j];
-        hE = H[H_EINT + l6];
+        if constexpr (STF != 1) load_hist();
         hvalid = hv != 0.0;
         kap_old = (int)hk;
         if (hvalid) {
@@ -2943,12 +2952,12 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
             if (km == 15) {  // stateless mask 15: the four-contact stance form
                 double hrow[12], gsv = 0.0;
                 ok = stance_reduce<true>(a, rb, P, pr, lane, wr, s, hrow, gsv, nullptr) && rank6_factor(P, s, gsv, lane);
-                if (ok) solve16<true, false>(a, rb, q, lane, wr, P, s, St16(s, fric), 15, WBC_QP_OK);
+                if (ok) solve16<true, false, STF>(a, rb, q, lane, wr, P, s, St16(s, fric), 15, WBC_QP_OK);
             } else {
                 const St16 V(s, P, fric);
                 bool vac = false;
                 ok = reduce_general(a, rb, P, pr, lane, km, s, V, vac);
-                if (ok) solve16<true, true>(a, rb, q, lane, wr, P, s, V, km, vac ? WBC_QP_INFEASIBLE : WBC_QP_OK);
+                if (ok) solve16<true, true, STF>(a, rb, q, lane, wr, P, s, V, km, vac ? WBC_QP_INFEASIBLE : WBC_QP_OK);
             }
             if (!ok && wr) {  // as wbc_update_solve_kernel's fallback record
                 lds_sync();
@@ -2977,7 +2986,7 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
             double hrow[12], gsv = 0.0;
             if (stance_reduce<true>(a, rb, P, pr, lane, wr, s, hrow, gsv, nullptr) && rank6_factor(P, s, gsv, lane)) {
                 UST(a, rb, 11);
-                solve16<true, false>(a, rb, qp, lane, wr, P, s, St16(s, fric), 15, WBC_QP_OK);
+                solve16<true, false, STF>(a, rb, qp, lane, wr, P, s, St16(s, fric), 15, WBC_QP_OK);
                 return true;
             }
             return false;
@@ -2986,7 +2995,7 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
         bool vac = false;
         if (reduce_general(a, rb, P, pr, lane, kap, s, V, vac)) {
             UST(a, rb, 11);
-            solve16<true, true>(a, rb, qp, lane, wr, P, s, V, kap, vac ? WBC_QP_INFEASIBLE : WBC_QP_OK);
+            solve16<true, true, STF>(a, rb, qp, lane, wr, P, s, V, kap, vac ? WBC_QP_INFEASIBLE : WBC_QP_OK);
             return true;
         }
         return false;
@@ -4366,6 +4375,8 @@ __device__ __forceinline__ int xcd_block(int b, int n) {
     const int x = b & 7, i = b >> 3, per = n >> 3, rem = n & 7;  // XCD x runs per + (x < rem) blocks
     return x * per + min(x, rem) + i;
 }
+// Two instances: STF = 0 for stateless steps (no history code at all), 1 for stateful ones
+template <int STF>
 WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) {
     __shared__ UpdLds L;
     const int seg = (int)threadIdx.x / UPD_SUB, lane = (int)threadIdx.x % UPD_SUB;
@@ -4412,7 +4423,7 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) {
     stage_to_lds<LIMG_LEN>(reinterpret_cast<double*>(&L), a.limg, (int)threadIdx.x);
     if (__all(empty)) return;  // the unused tail of a device-built map (uniform)
     lds_sync();
-    const bool solved = update_phase<UPD_SUB, true>(a, row, qp, kap, lane, wr, L.u[seg], L.prob[seg], nullptr, L.model,
+    const bool solved = update_phase<UPD_SUB, true, LdsModel, false, STF>(a, row, qp, kap, lane, wr, L.u[seg], L.prob[seg], nullptr, L.model,
                                                     &L.fric[0], vin);
     // a QP whose reduction was not usable: its problem goes to work row qp, and the wave solves it
     // with the general 24-variable method right here (drain_fallbacks, the rare path; the wave's
@@ -4431,7 +4442,7 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) {
     }
     const unsigned long long fm = __ballot(fb && lane == 0);
     if (fm)
-        drain_fallbacks<0>((const KernelArgs*)__builtin_amdgcn_kernarg_segment_ptr(), fm, qp,
+        drain_fallbacks<2 + STF>((const KernelArgs*)__builtin_amdgcn_kernarg_segment_ptr(), fm, qp,
                            reinterpret_cast<SolveLds*>(&L));
 }
 
@@ -4455,7 +4466,7 @@ WBC_UPDATE_KERNEL_ATTR void wbc_modes_kernel(KernelArgs a) {
     stage_to_lds<LIMG_LEN>(reinterpret_cast<double*>(&L), a.limg, (int)threadIdx.x);
     lds_sync();
     unsigned fails = 0;
-    update_phase<UPD_SUB, true, LdsModel, true>(a, row, row * K + k0, a.mode_masks[k0] & 15, lane, wr, L.u[seg],
+    update_phase<UPD_SUB, true, LdsModel, true, 0>(a, row, row * K + k0, a.mode_masks[k0] & 15, lane, wr, L.u[seg],
                                                 L.prob[seg], nullptr, L.model, &L.fric[0], vin, c, &fails);
     for (int it = 0; it < M; ++it) {
         const unsigned long long fm = __ballot(wr && lane == 0 && ((fails >> it) & 1u));
@@ -4653,7 +4664,10 @@ extern "C" hipError_t wbc_launch_modes(const wbc::KernelArgs* a, hipStream_t st)
 extern "C" hipError_t wbc_launch_update_solve(const wbc::KernelArgs* a, hipStream_t st) {
     static_assert(wbc::UPD_RPW == wbc::QMAP_SEG, "the wave map's segments are the kernel's");
     if (a->nwaves <= 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(wbc::wbc_update_solve_kernel, dim3(a->nwaves), dim3(64), 0, st, *a);
+    if (a->stateful)
+        hipLaunchKernelGGL(wbc::wbc_update_solve_kernel<1>, dim3(a->nwaves), dim3(64), 0, st, *a);
+    else
+        hipLaunchKernelGGL(wbc::wbc_update_solve_kernel<0>, dim3(a->nwaves), dim3(64), 0, st, *a);
     return hipGetLastError();
 }
 extern "C" hipError_t wbc_launch_reset(double* hist, const uint8_t* mask, int batch, hipStream_t st) {

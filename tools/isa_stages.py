@@ -10,7 +10,7 @@ import collections
 import re
 import sys
 
-SYM = "_ZN3wbc23wbc_update_solve_kernelENS_10KernelArgsE"
+SYM = "_ZN3wbc23wbc_update_solve_kernelILi0EEEvNS_10KernelArgsE"  # the stateless instance
 
 
 def stage_ranges(src):
@@ -29,7 +29,7 @@ def stage_ranges(src):
     s19, s20, s12 = find(r"UST\(ka, rb, 19\)", sr), find(r"UST\(ka, rb, 20\)", sr), find(r"UST\(ka, rb, 12\)", sr)
     s21, s22, s13 = find(r"UST\(ka, rb, 21\)", sr), find(r"UST\(ka, rb, 22\)", sr), find(r"UST\(ka, rb, 13\)", sr)
     s14 = find(r"UST\(ka, rb, 14\)", sr)
-    r6 = find(r"^__device__ bool rank6_factor\(")
+    r6 = find(r"^__device__ (__forceinline__ )?bool rank6_factor\(")
     rg = find(r"^__device__ bool reduce_general\(")
     g20, g21, g22 = find(r"UST\(ka, rb, 20\)", rg), find(r"UST\(ka, rb, 21\)", rg), find(r"UST\(ka, rb, 22\)", rg)
     g14 = find(r"UST\(ka, rb, 14\)", rg)

@@ -33,8 +33,10 @@ def summarise(pmc_dir, prefix="wbc::wbc_"):
     for f in sorted(glob.glob(os.path.join(pmc_dir, "pass*_counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
             name = r["Kernel_Name"]
+            if name.startswith("void "):  # a template instance: "void wbc::wbc_update_solve_kernel<0>(...)"
+                name = name[len("void "):]
             if name.startswith(prefix):
-                short = name[len("wbc::"):].split("(")[0]
+                short = name[len("wbc::"):].split("(")[0].split("<")[0]  # instances of one kernel share a name
                 vals[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in vals.items()}, \
            {k: {c: len(v) for c, v in d.items()} for k, d in vals.items()}
