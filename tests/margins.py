@@ -18,9 +18,12 @@ _RECORDS = {}
 TAU = 1e-9        # tau against the oracle (cold, stateful, stress); worst 4.4e-11
 X = 1e-9          # x* against the oracle; worst 1.9e-11
 GRF = 2e-11       # ground reaction forces against the oracle; worst 8.1e-13
-SAME = 1e-11      # two engine paths that solve the same QP differently (forms, hot vs cold); worst 1.3e-13
 BITS = 1e-13      # two engine paths that should agree to a few ulps (kernels of one form); worst 2.4e-15
-INTERMEDIATE = {"W": 5e-12, "Mbar_b": 1e-12, "rsw": 1e-12}  # others 1e-13 (worst 3.9e-15)
+INTERMEDIATE = {"W": 5e-12, "Mbar_b": 1e-12, "rsw": 1e-12,  # others 1e-13 (worst 3.9e-15)
+                # kinematics and the J / Mbar_j blocks: within a few ulps (worst 6.7e-16)
+                **{k: 1e-14 for k in ("Jbar", "Jfeet", "Mbar_j", "com", "comvel", "pfeet", "pose", "vc", "vfeet", "r1")}}
+GOLD = 1e-12      # tau against the committed cold fixtures and ragged batches (worst 5.9e-14)
+REPLAY = 1e-13    # the C++ shim's replay of the golden trajectories (worst 6.2e-15)
 
 
 def _test_id():

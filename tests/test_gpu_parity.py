@@ -3,7 +3,7 @@
 Tolerances (fp64 everywhere; tests/margins.py, tightened in round 4 to 10-80x the worst error
 measured on MI355X, profiles/r04/parity_margins.json, well inside BASELINE.md's parity gate):
   intermediates (M, C nu, Jacobians, CoM, Mbar, Jbar, bbar, wrench, bounds): 1e-13 relative to
-    max(1, |value|) (W 5e-12, Mbar_b and rsw 1e-12) -- the kernel uses closed forms instead of the
+    max(1, |value|) (W 5e-12, Mbar_b and rsw 1e-12; the kinematics, Jbar and Mbar_j 1e-14) -- the kernel uses closed forms instead of the
     reference's dense LU inverses, so agreement is to rounding, not bitwise;
   x*  within 1e-9 * (1 + |x*|_inf);   tau within 1e-9 * (1 + |tau|_inf);  grf 2e-11;
   QP status identical.

@@ -67,9 +67,9 @@ def test_stance_path_equals_general_path():
         n = len(other["status"])
         assert np.array_equal(elim["status"][:n], other["status"])
         assert np.array_equal(elim["iters"][:n], other["iters"])
-        assert close(elim["tau"][:n], other["tau"], M.SAME, "tau")
-        assert close(elim["grf"][:n], other["grf"], M.SAME, "grf")
-        assert close(elim["x"][:n], other["x"], M.SAME, "x")
+        assert close(elim["tau"][:n], other["tau"], M.BITS, "tau")
+        assert close(elim["grf"][:n], other["grf"], M.BITS, "grf")
+        assert close(elim["x"][:n], other["x"], M.BITS, "x")
 
 
 @pytest.mark.parametrize("maker,B", [("stance_cold", 4096), ("stance_cold", 333)])

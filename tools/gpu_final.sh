@@ -30,5 +30,7 @@ step b1_probe 120 python tools/b1_probe.py 2000
 step batch_sweep 180 python tools/batch_sweep.py 50
 step ust_stance 120 env WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_istamps.so python tools/ust16.py stance_cold 4096
 step ust_rl 120 env WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_istamps.so python tools/ust16.py rl_random 8192
+step ust_trot 120 env WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_istamps.so python tools/ust16.py trot 4096
+step modes_sweep 180 python tools/modes_sweep.py 50
 tail -1 $O/bench.log
 echo final done
