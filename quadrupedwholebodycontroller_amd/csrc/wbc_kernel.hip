@@ -1837,14 +1837,16 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
                     double jc[N];
 #pragma unroll
                     for (int k = 0; k < N; ++k) jc[k] = Jl[k * JMS + i];
-                    if (l == ol) {
-#pragma unroll
-                        for (int k = 0; k < N; ++k) V.col[k] = sel3d(js, n0[k], n1[k], n2[k]);
-                    }
-                    lds_sync();
+                    // the row's normal from its id, as the loop below builds it (p numbers the rows
+                    // as pstar does): a friction face from the shared table, a torque row as +-Nt;
+                    // the same values lane ol holds as n0 / n1 / n2, without an LDS exchange
+                    const bool frc = js == 0;
+                    const int tq = frc ? 0 : p - 16;
+                    const double* nrow = frc ? &V.fric[FRIC_ROW(p)] : &V.Nt[(tq >> 1) * NTS];
+                    const double sgn = (frc || (tq & 1)) ? 1.0 : -1.0;
                     double np[N], nn = 0.0;
 #pragma unroll
-                    for (int k = 0; k < N; ++k) { np[k] = V.col[k]; nn = fma(np[k], np[k], nn); }
+                    for (int k = 0; k < N; ++k) { np[k] = sgn * nrow[k]; nn = fma(np[k], np[k], nn); }
                     double d2[N], rk, zn, zk, dq, jq;
                     direction(dot_col(jc, np), pos, d2, rk, zn, zk, dq, jq);
                     if (!(zn > 1e-26 * fmax(1.0, nn))) { fail = true; break; }  // dependent: reject
@@ -1911,7 +1913,10 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
         const unsigned b0 = (unsigned)(__ballot(w0 == m) >> sh) & 0xFFFFu;
         const unsigned b1 = (unsigned)(__ballot(w1 == m) >> sh) & 0xFFFFu;
         const unsigned b2 = (unsigned)(__ballot(w2 == m) >> sh) & 0xFFFFu;
-        pstar = b0 ? __builtin_ctz(b0) : (b1 ? 16 + __builtin_ctz(b1) : 32 + __builtin_ctz(b2 | 0x10000u));
+        // the three masks as one 49-bit word, lowest set bit first (as conditionals on b0 and b1
+        // the compiler branched per segment)
+        pstar = __builtin_ctzll((unsigned long long)b0 | ((unsigned long long)b1 << 16) |
+                                ((unsigned long long)(b2 | 0x10000u) << 32));
         up = 0.0;
     };
     if (!done) select();
@@ -1967,7 +1972,6 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
             // ballot of the lanes that hold it (one 4-step DPP chain; a 6-bit lane tag in the
             // mantissa needed a second chain to recover the exact value)
             const double t1 = seg16_min(vt);
-            const int l1 = __builtin_ctzll((__ballot(vt == t1) >> ((int)threadIdx.x & 48)) & 0xFFFFull);
             const double t2 = (zn > 1e-14) ? (-sps * fast_rcp(zn)) : 1e300;
             const double t = fmin(t1, t2);
             IST(3);  // step lengths
@@ -1976,7 +1980,11 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
                 done = true;
             } else {
                 const bool full = (t2 < 1e299 && t2 <= t1);
-                if (t2 < 1e299) { sp0 += t * cz0; sp1 += t * cz1; sp2 += t * cz2; x += t * zk; }
+                // the primal and slack step only when the new row has a direction (t2 finite), as
+                // a select: a zero step leaves them exactly as they were (branched, it cost an
+                // exec-mask block per pass)
+                const double ts = (t2 < 1e299) ? t : 0.0;
+                sp0 += ts * cz0; sp1 += ts * cz1; sp2 += ts * cz2; x += ts * zk;
                 if (l < q) u -= t * rk;
                 up += t;
                 if (full) {
@@ -1987,8 +1995,10 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
                     householder_add(pos, d2, rk, zn, zk, dq, jq);
                     IST(4);  // select + Householder add
                 } else {
-                    // drop slot l1: shift the active lists, then Givens deletion (givens_drop) with the
-                    // rotation of step k from the R column of the row now in slot k: (J^T n)[k, k+1]
+                    // drop slot l1 (the lowest lane holding t1; only this path needs it): shift the
+                    // active lists, then Givens deletion (givens_drop) with the rotation of step k
+                    // from the R column of the row now in slot k: (J^T n)[k, k+1]
+                    const int l1 = __builtin_ctzll((__ballot(vt == t1) >> ((int)threadIdx.x & 48)) & 0xFFFFull);
                     const int dropped = seg_shfl_i(act, l1);
                     if (l == (dropped & 15)) ab &= ~(1 << (dropped >> 4));
                     const double un = seg_shfl(u, l + 1);
