@@ -1764,20 +1764,20 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
         dq = seg_shfl(dj, pos);  // lane 12.. holds 0
         jq = (l >= N || pos >= N) ? 0.0 : Jl[i * JMS + (pos < N ? pos : 0)];
         {
-            double acc[4] = {0.0, 0.0, 0.0, 0.0}, zz[4] = {0, 0, 0, 0};
+            double acc[2] = {0.0, 0.0}, zz[2] = {0, 0};
 #pragma unroll
             for (int j = 0; j < N; ++j) {
-                acc[j & 3] += rinv[j] * d1[j];
-                zz[j & 3] += d2[j] * d2[j];
+                acc[j & 1] += rinv[j] * d1[j];
+                zz[j & 1] += d2[j] * d2[j];
             }
-            rk = (l < N) ? (acc[0] + acc[1]) + (acc[2] + acc[3]) : 0.0;
-            zn = (zz[0] + zz[1]) + (zz[2] + zz[3]);
+            rk = (l < N) ? acc[0] + acc[1] : 0.0;
+            zn = zz[0] + zz[1];
         }
         {
-            double acc[4] = {0.0, 0.0, 0.0, 0.0};
+            double acc[2] = {0.0, 0.0};
 #pragma unroll
-            for (int j = 0; j < N; ++j) acc[j & 3] += Jr[j] * d2[j];
-            zk = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+            for (int j = 0; j < N; ++j) acc[j & 1] += Jr[j] * d2[j];
+            zk = acc[0] + acc[1];
         }
     };
     // Householder add at slot pos: J <- J H on columns pos.. (row l: v . J_l = z_l - alpha J_l[pos]);
@@ -1939,10 +1939,12 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
                 const bool frc = pstar < 16;
                 const int tq = pstar - 16;
                 const double* nrow = frc ? &V.fric[FRIC_ROW(pstar)] : &V.Nt[(tq >> 1) * NTS];
-                double a4[4] = {0.0, 0.0, 0.0, 0.0};
+                // two chains per dot in the pass (not four: the pass is issue-bound, and each
+                // dot then ends in one add instead of three)
+                double a2[2] = {0.0, 0.0};
 #pragma unroll
-                for (int k = 0; k < N; ++k) a4[k & 3] = fma(jc[k], nrow[k], a4[k & 3]);
-                const double dn = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+                for (int k = 0; k < N; ++k) a2[k & 1] = fma(jc[k], nrow[k], a2[k & 1]);
+                const double dn = a2[0] + a2[1];
                 dj = ((l < N) ? ((frc || (tq & 1)) ? 1.0 : -1.0) : 0.0) * dn;
             }
             const double sps = seg_shfl(sel3d(js, sp0, sp1, sp2), ol);
@@ -1953,17 +1955,17 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
             // slack rates n . z of the lane's rows (z_m broadcast from lane m)
             double cz0, cz1, cz2;
             {
-                double z0[4] = {0, 0, 0, 0}, z1[4] = {0, 0, 0, 0}, z2[4] = {0, 0, 0, 0};
+                double z0[2] = {0, 0}, z1[2] = {0, 0}, z2[2] = {0, 0};
 #pragma unroll
                 for (int m = 0; m < N; ++m) {
                     const double zm = seg_bcast<16>(zk, m);
-                    z0[m & 3] += n0[m] * zm;
-                    z1[m & 3] += n1[m] * zm;
-                    z2[m & 3] += n2[m] * zm;
+                    z0[m & 1] += n0[m] * zm;
+                    z1[m & 1] += n1[m] * zm;
+                    z2[m & 1] += n2[m] * zm;
                 }
-                cz0 = (z0[0] + z0[1]) + (z0[2] + z0[3]);
-                cz1 = (z1[0] + z1[1]) + (z1[2] + z1[3]);
-                cz2 = (z2[0] + z2[1]) + (z2[2] + z2[3]);
+                cz0 = z0[0] + z0[1];
+                cz1 = z1[0] + z1[1];
+                cz2 = z2[0] + z2[1];
             }
             IST(2);  // slack rates
             // step: t1 (drop an active slot) or t2 (the new row becomes active)
