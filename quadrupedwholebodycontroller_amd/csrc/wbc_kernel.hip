@@ -1585,6 +1585,7 @@ __device__ bool reduce_general([[maybe_unused]] const KernelArgs& ka, [[maybe_un
     // R7: H = L L^T, M = L^-1, x0 = -H^-1 g (ps.L, ps.xs: over W .. Si, all read by now)
     lds_sync();
     ok = factor12_rows(hrow, gsv, lane, &s.ps.L[0][0], s.ps.xs);
+    UST(ka, rb, 23);  // R7 done (diagnostic build)
     if (!ok) return false;
     // R8: torque map row r = i, t0_r, the row's reference-space norm; then Nt over Jbj
     {

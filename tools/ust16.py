@@ -42,6 +42,8 @@ res["general: R1-R4 (leg inverses, S6, S6^-1, Y, B, v, rho0)"] = med(t10, st(20)
 res["general: R5 (V, gamma, o, blk)"] = med(st(20), st(21), gen)
 res["general: R6 (H rows, g)"] = med(st(21), st(22), gen)
 res["general: R7 factor12 + R8 Nt"] = med(st(22), st(14), gen)
+res["general:   R7 factor12"] = med(st(22), st(23), gen)
+res["general:   R8 Nt"] = med(st(23), st(14), gen)
 res["prologue (kernel entry -> update start: model staging, input loads)"] = float(np.median((st(0) - st(30))[ok]))
 res["stance: reduce + rank-6 factor"] = med(t10, t11, stn)
 for n, (i0, i1) in (("leg inverses, W", (None, 19)), ("S", (19, 20)), ("S^-1", (20, 12)), ("Y, q0", (12, 21)),
