@@ -194,42 +194,15 @@ hipError_t upload_qmap(wbc_engine* h, const uint8_t* masks) {
 // on MI355X, 103.5 -> 112.3 M solves/s on the headline config without it).
 hipError_t drain(wbc_engine* h) { return h->stream ? hipStreamSynchronize(h->stream) : hipSuccess; }
 
-// Mode hypotheses per wave (KernelArgs::mloop, wbc_modes_kernel): the largest M dividing K that
-// still gives every SIMD of the device a wave (ceil(S / 4) K / M >= 4 CUs); 1, one hypothesis per
-// segment, when even that leaves SIMDs idle.  WBC_MODES_M (a divisor of K) overrides it (A/B runs,
-// tests).  The hypotheses go to the K / M chunks longest first, each to the chunk with the least
-// estimated work so far (LPT), so the chunks' waves end together: the estimate is a reduction and
-// solve of 30 units plus 3 per expected working-set pass (0.3, 2.3, 4.5, 6.7, 8.9
-// passes for 0 .. 4 stance legs).
+// Mode hypotheses per wave and their order (wbc_layout.h mode_loop_plan) for this engine's batch
+// and device: every SIMD (4 per CU) should get a wave.  WBC_MODES_M (a divisor of K) overrides M
+// (A/B runs, tests).
 void plan_mode_loop(wbc_engine* h, const uint8_t* modes, int32_t K) {
     const int64_t groups = (h->batch / K + 3) / 4;
     int cus = 256;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || cus <= 0) cus = 256;
-    int M = 1;
-    for (int m = K; m > 1; --m)
-        if (K % m == 0 && groups * (K / m) >= 4LL * cus) { M = m; break; }
-    if (const char* e = std::getenv("WBC_MODES_M")) {
-        const int m = std::atoi(e);
-        if (m >= 1 && m <= K && K % m == 0) M = m;
-    }
-    static const double passes[5] = {0.3, 2.3, 4.5, 6.7, 8.9};
-    const int C = K / M;
-    int idx[16], fill[16] = {};
-    double load[16] = {};
-    for (int k = 0; k < K; ++k) idx[k] = k;
-    auto cost = [&](int k) { return 30.0 + 3.0 * passes[__builtin_popcount(modes[k] & 15)]; };
-    std::stable_sort(idx, idx + K, [&](int x, int y) { return cost(x) > cost(y); });
-    uint8_t chunk[16][16];
-    for (int t = 0; t < K; ++t) {
-        int best = -1;
-        for (int c = 0; c < C; ++c)
-            if (fill[c] < M && (best < 0 || load[c] < load[best])) best = c;
-        chunk[best][fill[best]++] = (uint8_t)idx[t];
-        load[best] += cost(idx[t]);
-    }
-    for (int c = 0; c < C; ++c)
-        for (int i = 0; i < M; ++i) h->mode_order[c * M + i] = chunk[c][i];
-    h->mode_loop = M;
+    const char* e = std::getenv("WBC_MODES_M");
+    h->mode_loop = wbc::mode_loop_plan(modes, K, groups, 4LL * cus, e ? std::atoi(e) : 0, h->mode_order);
 }
 
 int64_t count_stance(const uint8_t* masks, size_t n) {

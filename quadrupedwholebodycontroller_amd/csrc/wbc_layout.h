@@ -270,5 +270,41 @@ inline int qmap_build(const uint8_t* masks, int B, int32_t* map) {
 }
 
 
+
+// Mode hypotheses per wave (KernelArgs::mloop, wbc_modes_kernel) for K hypotheses over `groups`
+// four-state groups on a device with `simds` SIMDs: the largest M dividing K that still gives
+// every SIMD a wave (groups K / M >= simds), 1 (one hypothesis per segment) when even that leaves
+// SIMDs idle; m_override (a divisor of K; 0 = none) replaces it.  order[c M .. c M + M - 1] are
+// chunk c's hypotheses: longest first, each to the chunk with the least estimated work so far
+// (LPT), the estimate a reduction and solve of 30 units plus 3 per expected working-set pass
+// (0.3, 2.3, 4.5, 6.7, 8.9 passes for 0 .. 4 stance legs).  Returns M.
+inline int mode_loop_plan(const uint8_t* modes, int K, int64_t groups, int64_t simds, int m_override,
+                          uint8_t* order) {
+    int M = 1;
+    for (int m = K; m > 1; --m)
+        if (K % m == 0 && groups * (K / m) >= simds) { M = m; break; }
+    if (m_override >= 1 && m_override <= K && K % m_override == 0) M = m_override;
+    static const double passes[5] = {0.3, 2.3, 4.5, 6.7, 8.9};
+    const int C = K / M;
+    int idx[16], fill[16] = {};
+    double load[16] = {};
+    for (int k = 0; k < K; ++k) idx[k] = k;
+    auto cost = [&](int k) { return 30.0 + 3.0 * passes[__builtin_popcount(modes[k] & 15u)]; };
+    for (int a = 1; a < K; ++a)  // stable insertion sort, costliest first
+        for (int b = a; b > 0 && cost(idx[b]) > cost(idx[b - 1]); --b) {
+            const int t = idx[b]; idx[b] = idx[b - 1]; idx[b - 1] = t;
+        }
+    uint8_t chunk[16][16];
+    for (int t = 0; t < K; ++t) {
+        int best = -1;
+        for (int c = 0; c < C; ++c)
+            if (fill[c] < M && (best < 0 || load[c] < load[best])) best = c;
+        chunk[best][fill[best]++] = (uint8_t)idx[t];
+        load[best] += cost(idx[t]);
+    }
+    for (int c = 0; c < C; ++c)
+        for (int i = 0; i < M; ++i) order[c * M + i] = chunk[c][i];
+    return M;
+}
 }  // namespace wbc
 #endif

@@ -113,3 +113,4 @@ def test_update_solve_split_equals_fused():
     for rows, tag, tols in ((~st & ok, "general", (M.BITS * 10, M.BITS, M.BITS)), (st & ok, "stance", (M.BITS, M.BITS, M.BITS))):
         for k, tol in zip(("tau", "grf", "x"), tols):
             assert M.close(fused[k][rows], split[k][rows], tol, f"{k} fused vs split ({tag} rows)"), (k, tag)
+
