@@ -114,3 +114,21 @@ def test_update_solve_split_equals_fused():
         for k, tol in zip(("tau", "grf", "x"), tols):
             assert M.close(fused[k][rows], split[k][rows], tol, f"{k} fused vs split ({tag} rows)"), (k, tag)
 
+
+def test_half_turn_poses_match_oracle():
+    """Base orientations whose rotation matrix has exact zeros where the RPY angles read it: half turns
+    about z, x and y and their compositions (quaternions with entries in {0, +-1}, and two tilted
+    yaws of pi).  At a half turn atan2 sees (+-0, x < 0): the engine's sign of that zero must give
+    the oracle's angle (atan2_br and -fno-signed-zeros), or the pose error flips by 2 pi.
+    Checked on the pose intermediate and the whole step."""
+    base = workloads.stance_cold(12, seed=31)
+    s = np.sqrt(0.5)
+    quats = [(0, 0, 1, 0), (1, 0, 0, 0), (0, 1, 0, 0), (0, 0, -1, 0), (-1, 0, 0, 0), (0, -1, 0, 0),
+             (0, 0, 0, 1), (0, 0, 0, -1), (0, s, s, 0), (s, 0, 0, s), (0.1, 0, 0.99498743710662, 0),
+             (0, 0.1, 0.99498743710662, 0)]  # (no pitch of +-pi/2: roll and yaw are rounding noise there)
+    for b, q in enumerate(quats):
+        base["base_pose"][b, 3:7] = q
+    out = run_engine(base)
+    ctrls = oracle_batch(base, range(len(quats)))
+    for b, c in enumerate(ctrls):
+        check_robot(c, out, b)
