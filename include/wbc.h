@@ -204,7 +204,12 @@ int32_t wbc_solve(wbc_engine* h, uint32_t flags);
  * slack rows included, the convention of a dense active set on the reference's 42 x 70 QP) under
  * WBC_SPLIT / WBC_FUSED.  WBC_QP_MAX_ITER is judged on that count against max_wsr, so near the cap
  * the default form (fewer changes for the same QP) can return WBC_QP_OK where the split / fused
- * forms return WBC_QP_MAX_ITER. */
+ * forms return WBC_QP_MAX_ITER.
+ * Every form picks the row to add as the most violated one by slack / |reference row|, with near-
+ * ties treated as ties: the lowest row id among the rows within WBC_TIE_BAND (relative) of the
+ * most violated, so the route (and `iters`) does not depend on rounding when two rows are violated
+ * alike in exact arithmetic.  The C oracle (oracle/wbc_ref.c) applies the same rule. */
+#define WBC_TIE_BAND 1e-9
 int32_t wbc_step(wbc_engine* h, uint32_t flags);
 int32_t wbc_synchronize(wbc_engine* h);
 

@@ -125,8 +125,9 @@ public:
     //   beforeCycle(iteration) [stands in for the subscriber callbacks], controlCycle() (= updateState,
     //   solveQP, computeJointTorques); stops when the QP fails (cpp:654-659) or after max_iterations.
     // rate_hz > 0 sleeps to that rate like ros::Rate; 0 runs back to back.  Returns iterations run.
-    // A direct call starts with ok() true (a requestShutdown() from an earlier loop or run() is
-    // cleared); a requestShutdown() during the loop ends it.
+    // A requestShutdown() before or during the loop ends it (ros::ok() turns false and stays false,
+    // cpp:648): the flag is not cleared on entry, so a shutdown requested before a control thread
+    // reaches this call is not lost.  resetShutdown() clears it for a new loop.
     long controlLoop(long max_iterations, double rate_hz = 0.0,
                      const std::function<void(long)>& beforeCycle = nullptr);
 
@@ -139,6 +140,7 @@ public:
     // Returns the cycles run.  Errors on the control thread (an engine failure) are rethrown here.
     long run();
     void requestShutdown() { shutdown_.store(true); }
+    void resetShutdown() { shutdown_.store(false); }
     bool ok() const { return !shutdown_.load(); }
     std::function<void()> spinOnce;
     std::function<void(long)> loopHook;

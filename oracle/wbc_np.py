@@ -40,6 +40,7 @@ NC = 6 + 3 * NL + 4 * NL + NJ + 6 * NL  # hpp:32
 INFTY = 1.0e20  # qpOASES::INFTY (used at cpp:508,512,514)
 
 QP_OK, QP_MAX_ITER, QP_INFEASIBLE, QP_NUMERIC = 0, 1, 2, 3
+TIE_BAND = 1e-9  # include/wbc.h WBC_TIE_BAND: near-ties in the row selection are ties (lowest id)
 
 
 # --------------------------------------------------------------------------------------
@@ -280,7 +281,10 @@ def gi_solve(H, g, CE, ce, CI, ci, max_iter=100):
         cand = np.where(viol < -tol)[0]
         if cand.size == 0:
             return x, QP_OK, iters, active
-        p = cand[np.argmin(viol[cand])]
+        # near-ties are ties: the lowest id within TIE_BAND of the most violated (include/wbc.h
+        # WBC_TIE_BAND, the engine's and the C oracle's rule)
+        vm = viol[cand].min()
+        p = cand[viol[cand] <= vm * (1.0 - TIE_BAND)][0]
         npv = CI[p]
         sp = s_all[p]
         up = 0.0

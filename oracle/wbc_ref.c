@@ -480,10 +480,15 @@ static int gi_solve(int n, const double* H, const double* g, int me, const doubl
         return (st_);                                                                  \
     } while (0)
     for (;;) {
-        /* most violated inactive inequality (scaled) */
+        /* most violated inactive inequality (scaled).  Near-ties are ties: the lowest row id among
+         * the rows within WBC_TIE_BAND (relative) of the most violated one, the rule the engine's
+         * kernels apply (wbc_kernel.hip solve16 / solve_phase / solve_stance), so rounding cannot
+         * send the two down different routes when two rows are violated alike in exact arithmetic
+         * (the +-x faces of a foot with f_x = 0) */
         int p = -1;
-        double best = 0.0;
+        double best = 0.0, wv[2 * NC];
         for (int i = 0; i < mi; ++i) {
+            wv[i] = 0.0;
             int isact = 0;
             for (int k = n_eq; k < q; ++k)
                 if (act[k] == i) { isact = 1; break; }
@@ -491,7 +496,15 @@ static int gi_solve(int n, const double* H, const double* g, int me, const doubl
             double s = -ci[i];
             for (int k = 0; k < n; ++k) s += CI[i * n + k] * x[k];
             double tol = tolv ? tolv[i] : 1e-10 * (fabs(ci[i]) > 1.0 ? fabs(ci[i]) : 1.0);
-            if (s < -tol && s / ni[i] < best) { best = s / ni[i]; p = i; }
+            if (s < -tol) {
+                wv[i] = s / ni[i];
+                if (wv[i] < best) best = wv[i];
+            }
+        }
+        if (best < 0.0) {
+            const double thr = best * (1.0 - WBC_TIE_BAND);
+            for (int i = 0; i < mi && p < 0; ++i)
+                if (wv[i] < 0.0 && wv[i] <= thr) p = i;
         }
         if (p < 0) { *iters_out = iters; GI_RETURN(WBC_REF_OK); }
         const double* np_ = CI + p * n;

@@ -146,15 +146,19 @@ int run_node(long cycles) {
     const long n = wbc.run();
     const auto tau = wbc.jointTorques();  // (a copy: the loop below publishes new torques)
     const int status = wbc.qpReturnValue();
-    // after run() ended by requestShutdown(), a direct controlLoop() starts with ok() true again
-    // (the shutdown request belonged to the finished loop) and runs its own cycles
-    const long again = wbc.controlLoop(25, 0.0, [&](long) {
+    auto feed = [&](long) {
         wbc.floatingBaseStateCallback(ms);
         wbc.jointStateCallback(js);
         wbc.referenceCallback(rm);
-    });
-    std::printf("{\"config\": \"node_run\", \"cycles\": %ld, \"control_loop_after_run\": %ld, \"qp_status\": %d, "
-                "\"messages\": %ld, \"tau\": [", n, again, status, sent.load());
+    };
+    // after run() ended by requestShutdown(), ok() stays false (ros::ok(), cpp:648): a direct
+    // controlLoop() runs no cycle until resetShutdown() clears the request
+    const long halted = wbc.controlLoop(25, 0.0, feed);
+    wbc.resetShutdown();
+    const long again = wbc.controlLoop(25, 0.0, feed);
+    std::printf("{\"config\": \"node_run\", \"cycles\": %ld, \"control_loop_after_shutdown\": %ld, "
+                "\"control_loop_after_run\": %ld, \"qp_status\": %d, "
+                "\"messages\": %ld, \"tau\": [", n, halted, again, status, sent.load());
     for (int i = 0; i < numberOfJoints; ++i) std::printf("%s%.9g", i ? ", " : "", tau[i]);
     std::printf("]}\n");
     return status == WBC_QP_OK && wbc.qpReturnValue() == WBC_QP_OK ? 0 : 3;

@@ -194,8 +194,7 @@ void WholeBodyController::terminate() {
 }
 
 long WholeBodyController::controlLoop(long max_iterations, double rate_hz, const std::function<void(long)>& beforeCycle) {
-    shutdown_.store(false);
-    return loop(max_iterations, rate_hz, beforeCycle);
+    return loop(max_iterations, rate_hz, beforeCycle);  // shutdown_ as the caller left it (resetShutdown)
 }
 
 long WholeBodyController::loop(long max_iterations, double rate_hz, const std::function<void(long)>& beforeCycle) {

@@ -679,8 +679,11 @@ int32_t enqueue_cycle(wbc_engine* h, uint32_t flags) {
     h->qmap_dev = qm;
     h->out_tau = bt; h->out_grf = bg; h->out_x = bx; h->out_status = bs; h->out_iters = bi;
     h->in_pose = ip; h->in_nu = in; h->in_qj = iq; h->in_ref = ir; h->in_contacts = ic; h->in_switching = is;
-    if (rc != WBC_OK) return rc;
+    // zero-copy: the pinned blocks hold this cycle's inputs (and map) whether or not the step ran, and
+    // the host-side mask count / map already describe them, so the own buffers follow them at the next
+    // sync_own in either case (on a failed step too, so d_contacts never lags n_stance_own / h_qmap)
     h->zc_stale = zc;
+    if (rc != WBC_OK) return rc;
     if (!zc)
         WBC_HIP(hipMemcpyAsync(h->h_out, h->d_outblk, (flags & WBC_NO_X) ? outb - xb : outb, hipMemcpyDeviceToHost,
                                h->stream));

@@ -306,6 +306,23 @@ __device__ __forceinline__ int wave_argmin_lane(double v) {
     return (mhi < 0) ? (63 - (mlo & 63)) : (mlo & 63);
 }
 
+// The row to add in the one-robot-per-wave solves (solve_phase, solve_stance): the exact minimum m
+// of v over the wave (the DPP min chain above without the lane tag), then the lowest lane whose v
+// lies within WBC_TIE_BAND of it (include/wbc.h: near-ties are ties, decided by the row id, as the
+// C oracle decides them).  v < 0 marks a violated row, 1e300 none; returns the lane (0 when m is
+// 1e300) and m (uniform).
+__device__ __forceinline__ int wave_select_band(double v, double& m) {
+    double w = dpp_min<0x128, 0xF>(v);  // row_ror:8
+    w = dpp_min<0x124, 0xF>(w);         // row_ror:4
+    w = dpp_min<0x122, 0xF>(w);         // row_ror:2
+    w = dpp_min<0x121, 0xF>(w);         // row_ror:1
+    w = dpp_min<0x142, 0xA>(w);         // row_bcast:15 into rows 1, 3
+    w = dpp_min<0x143, 0xC>(w);         // row_bcast:31 into rows 2, 3
+    m = bcast(w, 63);
+    const unsigned long long b = __ballot(v <= m * (1.0 - WBC_TIE_BAND));
+    return b ? __builtin_ctzll(b) : 0;
+}
+
 // Sum over the 16 lanes of each DPP row (row_ror 8, 4, 2, 1); lane 0's value is broadcast so the
 // result is uniform.  Used for the 13-body sums of the update phase (lanes >= 13 pass 0).
 __device__ __forceinline__ double row0_sum(double v) {
@@ -1662,7 +1679,8 @@ __device__ __forceinline__ int seg_shfl_i(int v, int j) {
 // default step's two instances, wbc_update_solve_kernel<STF>)
 template <bool ROWS, bool GEN, int STF = -1>
 __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, const Prob& P, UpdScratch& s,
-                        const St16& V, int kap, int status0) {
+                        const St16& V, int kap, int status0, double hws_lo = 0.0, double hws_hi = 0.0,
+                        double hws_tag = 0.0) {
     constexpr int N = 12;
     constexpr int NTS = GEN ? 12 : NTS_ST;  // Nt row stride
     const wbc_params& pr = a.pv;
@@ -1763,6 +1781,8 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
         // d[pos] and J[l][pos] (needed only by the Householder add, so their LDS latency is off
         // the chain): from lane pos of the segment and from the J mirror
         dq = seg_shfl(dj, pos);  // lane 12.. holds 0
+        // loaded unconditionally from a clamped address, then masked (a load under the lane
+        // condition is an exec-mask block with its own LDS wait)
         jq = (l >= N || pos >= N) ? 0.0 : Jl[i * JMS + (pos < N ? pos : 0)];
         {
             double acc[2] = {0.0, 0.0}, zz[2] = {0, 0};
@@ -1813,11 +1833,12 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
     // A dependent warm row or a multiplier below -1e-10 rejects the set: cold start from x0.
     if constexpr (GEN) {
         if (!done && (STF < 0 ? a.stateful != 0 : STF == 1) && !a.cold) {
-            const double* H = a.hist + (size_t)rb * HIST_LEN;
-            const double tag = H[H_WSKAP];
-            unsigned long long ws = (tag >= 16.0) ? ((unsigned long long)(unsigned)H[H_WSLO] |
-                                                     ((unsigned long long)(unsigned)H[H_WSHI] << 32))
-                                                  : 0ull;
+            // the previous set's words (H_WSLO, H_WSHI, H_WSKAP), loaded with the update's history
+            // batch (update_phase load_hist): read here, their HBM round trip sat on the chain of
+            // every stateful wave (~4 k ticks of the trot's ~7 k-tick hotstart stage)
+            unsigned long long ws = (hws_tag >= 16.0) ? ((unsigned long long)(unsigned)hws_lo |
+                                                         ((unsigned long long)(unsigned)hws_hi << 32))
+                                                      : 0ull;
             unsigned long long keep = 0xFFFFFFull << 16;  // torque rows
 #pragma unroll
             for (int lg = 0; lg < 4; ++lg)
@@ -1906,14 +1927,16 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
         const double w0 = (fon && !(ab & 1) && sp0 < -tol0) ? sp0 * in0 : 1e300;
         const double w1 = (!(ab & 2) && sp1 < -tol1) ? sp1 * in1 : 1e300;
         const double w2 = (v2 && !(ab & 4) && sp2 < -tol2) ? sp2 * in2 : 1e300;
-        // the exact minimum, then the lowest row id holding it from three ballots (friction rows
-        // 0..15 first, then 16 + l, then 32 + l: the oracle's strict-< scan order)
+        // the exact minimum, then the lowest row id within WBC_TIE_BAND of it (include/wbc.h:
+        // near-ties are ties) from three ballots (friction rows 0..15 first, then 16 + l, then
+        // 32 + l: the oracle's scan order)
         const double m = seg16_min(vmin_f64(w0, vmin_f64(w1, w2)));
         if (!(m < 1e299)) done = true;
+        const double thr = m * (1.0 - WBC_TIE_BAND);  // m < 0 when a row is violated
         const int sh = (int)threadIdx.x & 48;
-        const unsigned b0 = (unsigned)(__ballot(w0 == m) >> sh) & 0xFFFFu;
-        const unsigned b1 = (unsigned)(__ballot(w1 == m) >> sh) & 0xFFFFu;
-        const unsigned b2 = (unsigned)(__ballot(w2 == m) >> sh) & 0xFFFFu;
+        const unsigned b0 = (unsigned)(__ballot(w0 <= thr) >> sh) & 0xFFFFu;
+        const unsigned b1 = (unsigned)(__ballot(w1 <= thr) >> sh) & 0xFFFFu;
+        const unsigned b2 = (unsigned)(__ballot(w2 <= thr) >> sh) & 0xFFFFu;
         // the three masks as one 49-bit word, lowest set bit first (as conditionals on b0 and b1
         // the compiler branched per segment)
         pstar = __builtin_ctzll((unsigned long long)b0 | ((unsigned long long)b1 << 16) |
@@ -1928,7 +1951,13 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
         double jc[N];
 #pragma unroll
         for (int k = 0; k < N; ++k) jc[k] = Jl[k * JMS + i];
-        if (!done && ++iters > max_wsr) { status = WBC_QP_MAX_ITER; iters = max_wsr; done = true; }
+        {   // the working-set cap (++iters > max_wsr), as selects: branched, it cost two exec-mask
+            // blocks per pass
+            const bool hit = !done && iters >= max_wsr;
+            iters += (done || hit) ? 0 : 1;
+            status = hit ? WBC_QP_MAX_ITER : status;
+            done = done || hit;
+        }
         if (!done) {
             const int pos = q, ol = pstar & 15, js = pstar >> 4;
             // dj = column j of J . n for the chosen row, from the row id alone (no exchange of its
@@ -1939,7 +1968,10 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
             {
                 const bool frc = pstar < 16;
                 const int tq = pstar - 16;
-                const double* nrow = frc ? &V.fric[FRIC_ROW(pstar)] : &V.Nt[(tq >> 1) * NTS];
+                // the row as an offset from Nt, both candidates formed and one selected (a select
+                // of the two addresses compiled to two exec-mask blocks)
+                const int fo = (int)(V.fric - V.Nt) + FRIC_ROW(pstar), to = (tq >> 1) * NTS;
+                const double* nrow = V.Nt + (frc ? fo : to);
                 // two chains per dot in the pass (not four: the pass is issue-bound, and each
                 // dot then ends in one add instead of three)
                 double a2[2] = {0.0, 0.0};
@@ -2264,10 +2296,14 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
     // trip overlaps stages A-C; the others where the history is first used (after stage C).
     constexpr int NT = (18 + SUB - 1) / SUB;  // Tdot_inv columns per lane
     double hTd[18], hMa[NT][6], hR[3], hDo[3], hJo[12], hE = 0.0, hv = 0.0, hk = 15.0;
+    double hWlo = 0.0, hWhi = 0.0, hWtag = 0.0;  // the previous working set (solve16's hotstart)
     auto load_hist = [&]() {
         const int l6 = lane < 6 ? lane : 5, l12 = lane < 12 ? lane : 11;
         hv = H[H_VALID];
         hk = H[H_KOLD];
+        hWlo = H[H_WSLO];
+        hWhi = H[H_WSHI];
+        hWtag = H[H_WSKAP];
 #pragma unroll
         for (int cc = 0; cc < 18; ++cc) hTd[cc] = H[H_TDINV + l6 * 18 + cc];
 #pragma unroll
@@ -2970,7 +3006,8 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
                 const St16 V(s, P, fric);
                 bool vac = false;
                 ok = reduce_general(a, rb, P, pr, lane, km, s, V, vac);
-                if (ok) solve16<true, true, STF>(a, rb, q, lane, wr, P, s, V, km, vac ? WBC_QP_INFEASIBLE : WBC_QP_OK);
+                if (ok) solve16<true, true, STF>(a, rb, q, lane, wr, P, s, V, km, vac ? WBC_QP_INFEASIBLE : WBC_QP_OK,
+                                                 hWlo, hWhi, hWtag);
             }
             if (!ok && wr) {  // as wbc_update_solve_kernel's fallback record
                 lds_sync();
@@ -3008,7 +3045,8 @@ __device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int l
         bool vac = false;
         if (reduce_general(a, rb, P, pr, lane, kap, s, V, vac)) {
             UST(a, rb, 11);
-            solve16<true, true, STF>(a, rb, qp, lane, wr, P, s, V, kap, vac ? WBC_QP_INFEASIBLE : WBC_QP_OK);
+            solve16<true, true, STF>(a, rb, qp, lane, wr, P, s, V, kap, vac ? WBC_QP_INFEASIBLE : WBC_QP_OK, hWlo, hWhi,
+                                     hWtag);
             return true;
         }
         return false;
@@ -3690,8 +3728,9 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, const Pr
             if (pstar < 0) {  // most violated inequality (equalities are all active already)
                 double v = 1e300;
                 if (is_con && !is_eq && !active && sp < -tolv) v = sp * inrm;
-                const int idx = wave_argmin_lane(v);
-                if (!(bcast(v, idx) < 1e299)) break;  // no violated constraint: optimal
+                double vm;
+                const int idx = wave_select_band(v, vm);
+                if (!(vm < 1e299)) break;  // no violated constraint: optimal
                 pstar = idx;
                 up = 0.0;
             }
@@ -4056,8 +4095,9 @@ __device__ void solve_stance(const KernelArgs& a, int rb, const Prob* Pg, const 
             if (pstar < 0) {  // most violated row, by slack / |reference row|
                 double v = 1e300;
                 if (is_con && !active && sp < -tolv) v = sp * inrm;
-                const int idx = wave_argmin_lane(v);
-                if (!(bcast(v, idx) < 1e299)) break;  // no violated constraint: optimal
+                double vm;
+                const int idx = wave_select_band(v, vm);
+                if (!(vm < 1e299)) break;  // no violated constraint: optimal
                 pstar = idx;
                 up = 0.0;
             }

@@ -68,7 +68,9 @@ def test_controller_run_spins_callbacks_beside_the_control_thread():
     assert r.returncode == 0, r.stderr
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["cycles"] == 300 and res["qp_status"] == 0 and res["messages"] > 0
-    # a direct controlLoop() after run() (ended by requestShutdown) runs its own cycles
+    # after run() ended by requestShutdown, ok() stays false (ros::ok(), cpp:648): a direct
+    # controlLoop() runs nothing until resetShutdown(), then its own cycles
+    assert res["control_loop_after_shutdown"] == 0
     assert res["control_loop_after_run"] == 25
     s = subprocess.run([BIN, "stance", "300"], capture_output=True, text=True, timeout=300)
     ref = json.loads(s.stdout.strip().splitlines()[-1])

@@ -87,19 +87,20 @@ def test_cycle_keeps_bound_inputs():
         assert np.array_equal(got_a[k], want_a[k]), k
 
 
-def test_cycle_graph_replay_across_flag_and_mask_changes():
-    """wbc_cycle replays a captured graph while its flags, stream and masks allow (every mask equal);
-    flag changes re-capture it and mixed masks take the eager path with the wave map.  Every cycle must
-    equal the separate calls, stateful history included."""
+def test_cycle_zero_copy_across_flag_and_mask_changes():
+    """At B <= 64 wbc_cycle runs zero-copy: the step reads the pinned input block and the pinned wave
+    map and writes the pinned output block.  Stateful trot with mixed masks every
+    sixth cycle (the wave map path) and x switched on and off: every cycle must equal the separate
+    calls, history included."""
     B = 8
     seq = list(workloads.trot_sequence(B, steps=24, seed=9))
     e1, e2 = Engine(B), Engine(B)
     g = np.random.default_rng(2)
     for t, s in enumerate(seq):
         s = dict(s)
-        if t % 6 == 5:  # mixed masks: the eager path (wave map upload)
+        if t % 6 == 5:  # mixed masks: the wave map (built at copy time, read through its device address)
             s["contacts"] = g.integers(0, 16, B).astype(np.uint8)
-        flags = 0  # stateful throughout; x on / off alternates below (a re-capture each change)
+        flags = 0  # stateful throughout; x on / off alternates below
         want = separate_calls(e1, s, flags)
         got = e2.cycle(s["base_pose"], s["nu"], s["qj"], s["ref"], s["contacts"], s["switching"], flags,
                        want_x=(t % 3 != 0))
@@ -108,3 +109,27 @@ def test_cycle_graph_replay_across_flag_and_mask_changes():
         if t % 3 != 0:
             assert np.array_equal(got["x"], want["x"]), t
     e1.close(); e2.close()
+
+
+@pytest.mark.parametrize("B", [8, 24])
+def test_zero_copy_cycle_then_plain_step_mixed_masks(B):
+    """After a zero-copy cycle with mixed masks the engine's own device inputs, outputs and wave map
+    are brought up to date lazily (sync_own) before any other call.  outputs() right after the cycle,
+    then a plain wbc_step on the cycle's inputs and outputs() again, must give exactly what the
+    separate calls give (stateless and stateful)."""
+    a = workloads.rl_random(B, seed=70 + B)
+    for flags in (STATELESS, 0):
+        ref = Engine(B)
+        want = separate_calls(ref, a, flags)
+        want2 = (ref.step(flags), ref.outputs())[1]  # the second cycle of the same inputs (history)
+        ref.close()
+        e = Engine(B)
+        got = e.cycle(a["base_pose"], a["nu"], a["qj"], a["ref"], a["contacts"], a["switching"], flags)
+        after = e.outputs()  # the cycle's outputs, now read from the engine's own buffers
+        e.step(flags)  # the cycle's inputs, masks and map from the engine's own buffers
+        got2 = e.outputs()
+        e.close()
+        for k in KEYS:
+            assert np.array_equal(got[k], want[k]), (flags, k)
+            assert np.array_equal(after[k], want[k]), (flags, k)
+            assert np.array_equal(got2[k], want2[k]), (flags, k)
