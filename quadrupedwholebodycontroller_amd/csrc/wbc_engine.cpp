@@ -367,7 +367,7 @@ int32_t wbc_create(const wbc_model* model, const wbc_params* params, int32_t bat
     ALLOC(d_work, B * wbc::WORK_LEN);
     ALLOC(d_fb, 2 + B);
     ALLOC(d_dbg, B * WBC_DBG_LEN);
-    ALLOC(d_qmap, wbc::qmap_capacity(batch));
+    ALLOC(d_qmap, wbc::qmap_capacity(batch) + wbc::qmap_scratch(batch));  // + the device builder's scratch
 #undef ALLOC
     if (hipHostMalloc(&h->h_qmap, sizeof(int32_t) * wbc::qmap_capacity(batch), hipHostMallocMapped) != hipSuccess) {
         wbc_destroy(h);

@@ -1845,7 +1845,95 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
                 if ((kap >> lg) & 1) keep |= 0xFull << (4 * lg);
             ws &= keep;
             const int nw = __popcll(ws);
-            if (nw > 0 && nw <= N) {
+            // Direct check for a warm set of one or two rows (the trot's: 88 % of its QPs carry no
+            // row, 12 % one, < 1 % two): the point where the rows hold, x = x0 + J0 D lambda with
+            // D = J0^T N_A (the J mirror's columns still hold J0), G = D^T D, G lambda = -s_A(x0),
+            // straight from the 1 x 1 / 2 x 2 system instead of Householder re-adds through the
+            // mirror and 12 segment sums for R^-T s_A (~5 k ticks per stateful wave).  Accepted when
+            // the rows are independent (the re-add's test), every multiplier >= -1e-10 (its
+            // rejection rule) and no other row is violated at x: the set is then optimal, exactly
+            // what the block below would find after its re-adds (iters 0, the same working set), so
+            // the segment is done.  Anything else takes the block below unchanged.
+            bool direct_ok = false, warm_pt = false, small_rej = false;
+            double ua = 0.0, ub = 0.0, xw = 0.0;  // the direct point's multipliers and x (warm_pt)
+            if (seg_any<16>(nw >= 1 && nw <= 2)) {
+                const unsigned long long r1w = ws & (ws - 1ull);
+                const int pa = __builtin_ctzll(ws | (1ull << 63)), pb = (nw == 2) ? __builtin_ctzll(r1w | (1ull << 63)) : pa;
+                double jc[N];
+#pragma unroll
+                for (int k = 0; k < N; ++k) jc[k] = Jl[k * JMS + i];
+                auto warm_row = [&](int p, double* np, double& nn) {
+                    const bool frc = p < 16;
+                    const int tq = p - 16;
+                    const int fo = (int)(V.fric - V.Nt) + FRIC_ROW(p & 15), to = ((tq < 0 ? 0 : tq) >> 1) * NTS;
+                    const double* nrow = V.Nt + (frc ? fo : to);
+                    const double sgn = (frc || (tq & 1)) ? 1.0 : -1.0;
+                    nn = 0.0;
+#pragma unroll
+                    for (int k = 0; k < N; ++k) { np[k] = sgn * nrow[k]; nn = fma(np[k], np[k], nn); }
+                };
+                double na[N], nb[N], nna, nnb;
+                warm_row(pa, na, nna);
+                warm_row(pb, nb, nnb);
+                const double da = dot_col(jc, na), db = (nw == 2) ? dot_col(jc, nb) : 0.0;  // D[l][0..1]
+                const double g11 = seg_sum<16>(da * da), g12 = seg_sum<16>(da * db), g22 = seg_sum<16>(db * db);
+                const double s_a = seg_shfl(sel3d(pa >> 4, sp0, sp1, sp2), pa & 15);
+                const double s_b = seg_shfl(sel3d(pb >> 4, sp0, sp1, sp2), pb & 15);
+                double la, lb;
+                bool ind;
+                if (nw == 2) {
+                    const double det = fma(g11, g22, -g12 * g12);
+                    ind = g11 > 1e-26 * fmax(1.0, nna) && det > 1e-26 * fmax(1.0, nnb) * g11;
+                    const double idt = fast_rcp(ind ? det : 1.0);
+                    la = fma(s_b, g12, -s_a * g22) * idt;
+                    lb = fma(s_a, g12, -s_b * g11) * idt;
+                } else {
+                    ind = g11 > 1e-26 * fmax(1.0, nna);
+                    la = -s_a * fast_rcp(ind ? g11 : 1.0);
+                    lb = 0.0;
+                }
+                bool ok = nw >= 1 && nw <= 2 && ind && la >= -1e-10 && lb >= -1e-10;
+                // x = x0 + J0 e, e = D lambda (e_k in lane k)
+                const double ek = fma(da, la, db * lb);
+                double xd = 0.0;
+                {
+                    double a2[2] = {0.0, 0.0};
+#pragma unroll
+                    for (int k = 0; k < N; ++k) a2[k & 1] = fma(Jr[k], seg_bcast<16>(ek, k), a2[k & 1]);
+                    xd = (l < N) ? x + (a2[0] + a2[1]) : 0.0;
+                }
+                const double t0s = sp0, t1s = sp1, t2s = sp2;
+                {
+                    double xv[N];
+#pragma unroll
+                    for (int j = 0; j < N; ++j) xv[j] = seg_bcast<16>(xd, j);
+                    slacks(xv);
+                }
+                int abd = 0;
+                if (l == (pa & 15)) abd |= 1 << (pa >> 4);
+                if (nw == 2 && l == (pb & 15)) abd |= 1 << (pb >> 4);
+                const bool viol = (fon && !(abd & 1) && sp0 < -tol0) || (!(abd & 2) && sp1 < -tol1) ||
+                                  (v2 && !(abd & 4) && sp2 < -tol2);
+                const bool any_viol = seg_any<16>(viol);
+                direct_ok = ok && !any_viol;
+                // rows violated at the warm point: the set's Householder re-adds (J and R for the loop)
+                // below, but the point, its multipliers and slacks are these; a rejected set (dependent
+                // rows or a multiplier < -1e-10) starts cold from x0, as the block below would after
+                // its re-adds, without them
+                warm_pt = ok && any_viol;
+                small_rej = (nw >= 1 && nw <= 2) && !ok;
+                if (direct_ok) {
+                    x = xd;
+                    ab = abd;
+                    done = true;  // optimal: no row to add (iters 0, status OK)
+                } else if (!warm_pt) {
+                    sp0 = t0s; sp1 = t1s; sp2 = t2s;
+                }
+                ua = fmax(la, 0.0);
+                ub = fmax(lb, 0.0);
+                xw = xd;
+            }
+            if (nw > 0 && nw <= N && !direct_ok && !small_rej) {
                 if (l < N) {  // J0 for a rejection
 #pragma unroll
                     for (int j = 0; j < N; j += 2) *reinterpret_cast<double2*>(&V.J0[i * 12 + j]) = make_double2(Jr[j], Jr[j + 1]);
@@ -1878,7 +1966,10 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
                     ++q;
                     mirror();
                 }
-                if (!fail) {
+                if (!fail && warm_pt) {  // the direct point: slots 0, 1 hold the rows in ctz order
+                    if (l < q) u = (l == 0) ? ua : ub;
+                    x = xw;
+                } else if (!fail) {
                     // slack at x0 of the row in slot l (from its owner lane), then v, u, x
                     const int ow = act < 0 ? 0 : act & 15, jw = act < 0 ? 0 : act >> 4;
                     const double o0 = seg_shfl(sp0, ow), o1 = seg_shfl(sp1, ow), o2 = seg_shfl(sp2, ow);
@@ -1921,6 +2012,7 @@ __device__ void solve16(const KernelArgs& a, int rb, int qp, int l, bool wr, con
         }
     }
 
+    UST(a, rb, 25);  // hotstart block (stateful general form; immediate otherwise)
     // most violated row, by slack / |reference row| (ties to the lowest row); none: optimal.  Run
     // before the loop and then right after each add, where it overlaps the Householder update of J
     auto select = [&]() {
@@ -4613,28 +4705,90 @@ void wbc_solve_stance_kernel(KernelArgs a) {
 
 // The default step's wave map for device-bound contact masks (KernelArgs::qmap, under WBC_GROUP):
 // the layout of qmap_build (wbc_layout.h qmap_plan / qmap_pos), then QMAP_EMPTY up to the capacity,
-// so the step launches qmap_capacity(B) / 4 workgroups without reading the masks back.  One
-// workgroup: thread t counts and later places robots [t C, (t + 1) C) with its own LDS column of
-// per-mask counts, the columns are scanned per mask over the threads.
+// so the step launches qmap_capacity(B) / 4 workgroups without reading the masks back.  Three
+// launches over blocks of QMAP_BLOCK QPs (the first version, one workgroup walking every mask
+// twice, took 20 us at B = 8192 and 130 us at B = 65536, more than the grouping saved there,
+// profiles/r05/qmap):
+//   wbc_qmap_count    per block: the count and first QP of each mask (one ballot per mask and wave
+//                     round of 64 QPs);
+//   wbc_qmap_plan     one workgroup: each mask's exclusive prefix over the blocks, the totals and the
+//                     plan (qmap_plan);
+//   wbc_qmap_scatter  per block: each QP's rank in its mask's bucket (its block's prefix, the earlier
+//                     waves' and rounds' counts, its ballot's mbcnt) and its entry at qmap_pos; the
+//                     padding entries and QMAP_EMPTY up to the capacity.
+// Buckets keep batch order, as the host builder's (tests/test_gpu_grouping.py: bit-identical steps).
 constexpr int QMAP_THREADS = 256;
-__global__ __launch_bounds__(QMAP_THREADS) void wbc_qmap_kernel(const uint8_t* masks, int B, int32_t* map, int cap) {
-    __shared__ int col[16][QMAP_THREADS];  // counts, then inclusive prefixes over the threads
-    __shared__ int tot[16], first[16];
-    __shared__ QmapPlan plan;
-    const int t = (int)threadIdx.x;
-    const int C = (B + QMAP_THREADS - 1) / QMAP_THREADS, b0 = min(t * C, B), b1 = min(b0 + C, B);
+static_assert(sizeof(QmapPlan) <= 64 * sizeof(int), "the plan fits the scratch tail (qmap_scratch)");
+static_assert(QMAP_BLOCK == 4 * QMAP_THREADS, "four rounds of 64 QPs per wave");
+// per wave of the block: its 256 QPs in four rounds of 64, ballot per mask; counts and the first QP
+__device__ __forceinline__ void qmap_wave_counts(const uint8_t* masks, int B, int b0, int* c, int* f) {
+    const int l = (int)threadIdx.x & 63;
 #pragma unroll
-    for (int m = 0; m < 16; ++m) col[m][t] = 0;
-    if (t < 16) first[t] = B;
-    __syncthreads();
-    for (int b = b0; b < b1; ++b) {
-        const int m = masks[b] & 15;
-        if (col[m][t]++ == 0) atomicMin(&first[m], b);
+    for (int k = 0; k < 16; ++k) { c[k] = 0; f[k] = -1; }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int b = b0 + 64 * r + l;
+        const int m = b < B ? (masks[b] & 15) : 16;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const unsigned long long bal = __ballot(m == k);
+            c[k] += __popcll(bal);
+            if (f[k] < 0 && bal) f[k] = b0 + 64 * r + __builtin_ctzll(bal);
+        }
+    }
+}
+__global__ __launch_bounds__(QMAP_THREADS) void wbc_qmap_count(const uint8_t* masks, int B, int* scr) {
+    __shared__ int wc[4][16], wf[4][16];
+    const int w = (int)threadIdx.x >> 6, l = (int)threadIdx.x & 63;
+    int c[16], f[16];
+    qmap_wave_counts(masks, B, (int)blockIdx.x * QMAP_BLOCK + 256 * w, c, f);
+    if (l == 0) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) { wc[w][k] = c[k]; wf[w][k] = f[k]; }
     }
     __syncthreads();
-    int own[16];  // this thread's counts (the exclusive prefix is the inclusive one minus these)
+    const int t = (int)threadIdx.x;
+    if (t < 16) {
+        int n = 0, fi = -1;
+        for (int ww = 0; ww < 4; ++ww) {
+            n += wc[ww][t];
+            if (fi < 0) fi = wf[ww][t];
+        }
+        scr[blockIdx.x * 32 + t] = n;
+        scr[blockIdx.x * 32 + 16 + t] = fi;
+    }
+}
+__global__ __launch_bounds__(QMAP_THREADS) void wbc_qmap_plan(int B, int* scr) {
+    __shared__ int col[16][QMAP_THREADS];  // per-thread sums, then inclusive prefixes over the threads
+    __shared__ int first[16];
+    const int t = (int)threadIdx.x, nb = qmap_blocks(B);
+    const int C = (nb + QMAP_THREADS - 1) / QMAP_THREADS, j0 = min(t * C, nb), j1 = min(j0 + C, nb);
+    if (t < 16) first[t] = -1;
+    // this thread's blocks: counts and the first QP of each mask (its lowest block holding the mask).
+    // One block per thread up to 256 blocks: all 32 loads issued together (a load, a wait and an LDS
+    // atomic per mask took 10-25 us, profiles/r05/qmap)
+    int own[16], fst[16];
+    if (j1 - j0 == 1) {
 #pragma unroll
-    for (int m = 0; m < 16; ++m) own[m] = col[m][t];
+        for (int m = 0; m < 16; ++m) {
+            own[m] = scr[j0 * 32 + m];
+            fst[m] = scr[j0 * 32 + 16 + m];
+        }
+    } else {
+#pragma unroll
+        for (int m = 0; m < 16; ++m) { own[m] = 0; fst[m] = -1; }
+        for (int j = j0; j < j1; ++j) {
+#pragma unroll
+            for (int m = 0; m < 16; ++m) {
+                const int n = scr[j * 32 + m], f = scr[j * 32 + 16 + m];
+                if (fst[m] < 0 && n > 0) fst[m] = f;
+                own[m] += n;
+            }
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < 16; ++m) col[m][t] = own[m];
+    __syncthreads();
     for (int d = 1; d < QMAP_THREADS; d <<= 1) {  // Hillis-Steele, all masks per step
         int v[16];
 #pragma unroll
@@ -4644,31 +4798,78 @@ __global__ __launch_bounds__(QMAP_THREADS) void wbc_qmap_kernel(const uint8_t* m
         for (int m = 0; m < 16; ++m) col[m][t] += v[m];
         __syncthreads();
     }
-    if (t < 16) tot[t] = col[t][QMAP_THREADS - 1];
+    // the first thread holding mask m (exclusive prefix 0, own count > 0) holds its first QP; the
+    // blocks' exclusive prefixes go in place of their counts (no re-read for one block per thread)
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        const int ex = col[m][t] - own[m];
+        if (own[m] > 0 && ex == 0) first[m] = fst[m];
+    }
+    if (j1 - j0 == 1) {
+#pragma unroll
+        for (int m = 0; m < 16; ++m) scr[j0 * 32 + m] = col[m][t] - own[m];
+    } else {
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            int run = col[m][t] - own[m];
+            for (int j = j0; j < j1; ++j) {
+                const int n = scr[j * 32 + m];
+                scr[j * 32 + m] = run;
+                run += n;
+            }
+        }
+    }
     __syncthreads();
     if (t == 0) {
-        int f[16];
-        for (int m = 0; m < 16; ++m) f[m] = first[m] < B ? first[m] : -1;
-        qmap_plan(tot, f, plan);
+        int tot[16], f[16];
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            tot[m] = col[m][QMAP_THREADS - 1];
+            f[m] = first[m];
+        }
+        QmapPlan p;
+        qmap_plan(tot, f, p);
+        *reinterpret_cast<QmapPlan*>(scr + 32 * nb) = p;
+    }
+}
+__global__ __launch_bounds__(QMAP_THREADS) void wbc_qmap_scatter(const uint8_t* masks, int B, const int* scr,
+                                                                 int32_t* map, int cap) {
+    __shared__ int wc[4][16];
+    const int w = (int)threadIdx.x >> 6, l = (int)threadIdx.x & 63, nb = qmap_blocks(B);
+    const QmapPlan& plan = *reinterpret_cast<const QmapPlan*>(scr + 32 * nb);
+    const int b0 = (int)blockIdx.x * QMAP_BLOCK + 256 * w;
+    int c[16], f[16];
+    qmap_wave_counts(masks, B, b0, c, f);
+    if (l == 0) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) wc[w][k] = c[k];
     }
     __syncthreads();
-    int j[16];
+    int base[16];
 #pragma unroll
-    for (int m = 0; m < 16; ++m) j[m] = col[m][t] - own[m];
-    for (int b = b0; b < b1; ++b) {
-        const int m = masks[b] & 15;
-        int jm = 0;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {  // register select (a dynamic index would go to scratch)
-            jm = (k == m) ? j[k] : jm;
-            j[k] += (k == m);
-        }
-        map[qmap_pos(plan, m, jm)] = qmap_entry(b, m);
+    for (int k = 0; k < 16; ++k) {
+        int n = scr[blockIdx.x * 32 + k];
+        for (int ww = 0; ww < w; ++ww) n += wc[ww][k];
+        base[k] = n;
     }
-    const int used = 4 * plan.waves;
-    if (t < QMAP_SEG && plan.base1 && t >= plan.pad0) map[t] = plan.v0;
-    if (t >= QMAP_SEG && t < 2 * QMAP_SEG && plan.pad1 + t - QMAP_SEG < plan.end1) map[plan.pad1 + t - QMAP_SEG] = plan.v1;
-    for (int p = used + t; p < cap; p += QMAP_THREADS) map[p] = QMAP_EMPTY;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int b = b0 + 64 * r + l;
+        const int m = b < B ? (masks[b] & 15) : 16;
+        int j = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const unsigned long long bal = __ballot(m == k);
+            const int below = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+            if (m == k) j = base[k] + below;
+            base[k] += __popcll(bal);
+        }
+        if (b < B) map[qmap_pos(plan, m, j)] = qmap_entry(b, m);
+    }
+    const int gt = (int)blockIdx.x * QMAP_THREADS + (int)threadIdx.x;
+    if (gt < QMAP_SEG && plan.base1 && gt >= plan.pad0) map[gt] = plan.v0;
+    if (gt >= QMAP_SEG && gt < 2 * QMAP_SEG && plan.pad1 + gt - QMAP_SEG < plan.end1) map[plan.pad1 + gt - QMAP_SEG] = plan.v1;
+    for (int p = 4 * plan.waves + gt; p < cap; p += (int)gridDim.x * QMAP_THREADS) map[p] = QMAP_EMPTY;
 }
 
 __global__ void wbc_reset_kernel(double* hist, const uint8_t* mask, int batch) {
@@ -4686,9 +4887,15 @@ extern "C" hipError_t wbc_launch_step(const wbc::KernelArgs* a, hipStream_t st) 
     hipLaunchKernelGGL(wbc::wbc_step_kernel, dim3(a->batch), dim3(64), 0, st, *a);
     return hipGetLastError();
 }
+// map: qmap_capacity(batch) entries followed by qmap_scratch(batch) ints of scratch
 extern "C" hipError_t wbc_launch_qmap(const uint8_t* masks, int batch, int32_t* map, hipStream_t st) {
-    hipLaunchKernelGGL(wbc::wbc_qmap_kernel, dim3(1), dim3(wbc::QMAP_THREADS), 0, st, masks, batch, map,
-                       wbc::qmap_capacity(batch));
+    if (batch <= 0) return hipErrorInvalidValue;
+    const int cap = wbc::qmap_capacity(batch), nb = wbc::qmap_blocks(batch);
+    int* scr = map + cap;
+    hipLaunchKernelGGL(wbc::wbc_qmap_count, dim3(nb), dim3(wbc::QMAP_THREADS), 0, st, masks, batch, scr);
+    hipLaunchKernelGGL(wbc::wbc_qmap_plan, dim3(1), dim3(wbc::QMAP_THREADS), 0, st, batch, scr);
+    hipLaunchKernelGGL(wbc::wbc_qmap_scatter, dim3(nb), dim3(wbc::QMAP_THREADS), 0, st, masks, batch,
+                       static_cast<const int*>(scr), map, cap);
     return hipGetLastError();
 }
 extern "C" hipError_t wbc_launch_update(const wbc::KernelArgs* a, hipStream_t st) {

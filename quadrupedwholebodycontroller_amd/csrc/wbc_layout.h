@@ -209,6 +209,12 @@ constexpr uint8_t QMAP_ORDER[16] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13
 #endif
 // capacity of the map for B QPs (entries): ceil(B / 4) + 1 waves
 WBC_HD inline int qmap_capacity(int B) { return QMAP_SEG * ((B + QMAP_SEG - 1) / QMAP_SEG + 1); }
+// The device builder's scratch after the map (wbc_qmap_count / _plan / _scatter): per block of
+// QMAP_BLOCK QPs its 16 mask counts (then their exclusive prefixes over the blocks) and 16 first
+// indices, then the plan
+constexpr int QMAP_BLOCK = 1024;
+WBC_HD inline int qmap_blocks(int B) { return (B + QMAP_BLOCK - 1) / QMAP_BLOCK; }
+WBC_HD inline int qmap_scratch(int B) { return 32 * qmap_blocks(B) + 64; }
 struct QmapPlan {
     int base1, base2, waves;  // region 1 / 2 starts (entries), total waves
     int full[16];             // QPs of bucket m in whole waves (4 * floor(cnt / 4))
@@ -223,6 +229,7 @@ WBC_HD inline void qmap_plan(const int* cnt, const int* first, QmapPlan& p) {
     p.pad0 = r15;
     p.v0 = ~qmap_entry(first[15] < 0 ? 0 : first[15], 15);
     int o1 = 0, o2 = 0, last = -1;
+#pragma unroll  // (device builder: bucket m a constant, the plan's fields registers)
     for (int k = 0; k < 16; ++k) {
         const int m = QMAP_ORDER[k];
         p.full[m] = cnt[m] - cnt[m] % QMAP_SEG;

@@ -7,7 +7,7 @@ robot's outputs depend only on its own inputs, mask and flags, never on which ro
   own).
 * A robot solved inside a sub-batch (a shard, as on N ranks) equals the same robot in the full batch.
 * Device-bound masks equal host-copied masks, with the map built on the stream (WBC_GROUP,
-  wbc_qmap_kernel) and without one (waves of four consecutive, mixed-mask QPs: each segment takes
+  wbc_qmap_count / _plan / _scatter) and without one (waves of four consecutive, mixed-mask QPs: each segment takes
   its own form), also on a permuted batch.
 * Mask-15 robots in a mixed stateless batch take the four-contact stance form, as in an all-stance
   batch: bit-identical to the same robots stepped alone.
@@ -100,9 +100,9 @@ def test_stateful_permuted_bit_identical():
         eb.close()
 
 
-@pytest.mark.parametrize("group", [True, False])
-def test_device_bound_masks_equal_host_masks(group):
-    B = 2050
+@pytest.mark.parametrize("group,B", [(True, 2050), (False, 2050), (True, 16389)])
+def test_device_bound_masks_equal_host_masks(group, B):
+    """B = 16389: the device map builder over 17 blocks of 1024 QPs (wbc_qmap_count / _plan / _scatter)."""
     inp = workloads.straight_legs(workloads.rl_random(B, seed=27), every=9)
     a = run(inp, flags=STATELESS | NO_X)
     flags = STATELESS | NO_X | (GROUP if group else 0)

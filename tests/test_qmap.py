@@ -12,7 +12,7 @@ never depends on its wave-mates; the map only decides which QPs share a wave (DE
 * at most ceil(B / 4) + 1 waves (the capacity the device map is sized for);
 * a batch whose masks are all equal needs no map (0 waves).
 
-The device builder (wbc_qmap_kernel, for device-bound masks under WBC_GROUP) computes the same plan;
+The device builder (wbc_qmap_count / _plan / _scatter, for device-bound masks under WBC_GROUP) computes the same plan;
 the GPU test tests/test_gpu_grouping.py checks that both give bit-identical steps."""
 import os
 import subprocess

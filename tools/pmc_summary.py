@@ -42,11 +42,32 @@ def summarise(pmc_dir, prefix="wbc::wbc_"):
            {k: {c: len(v) for c, v in d.items()} for k, d in vals.items()}
 
 
-def traffic_bytes(mean):
-    """HBM bytes per launch: FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE, KiB -> bytes."""
+def traffic_bytes(mean, read_factor=2.0, write_factor=1.0):
+    """HBM bytes per launch: FETCH_SIZE x read_factor + WRITE_SIZE x write_factor, KiB -> bytes.
+    The defaults are the guide's figures for 16 B/lane streams (FETCH_SIZE counts half); the step's
+    own patterns have measured factors (calibration below)."""
     if "FETCH_SIZE" not in mean or "WRITE_SIZE" not in mean:
         return None
-    return 2.0 * mean["FETCH_SIZE"] * 1024.0 + mean["WRITE_SIZE"] * 1024.0
+    return read_factor * mean["FETCH_SIZE"] * 1024.0 + write_factor * mean["WRITE_SIZE"] * 1024.0
+
+
+# the calibration kernel (tools/micro/calib.hip) that reproduces each bench workload's access pattern
+CALIB_PATTERN = {"stance_cold": "calib_rows_stance", "rl_random": "calib_rows_rl", "modes16": "calib_rows_modes",
+                 "trot": "calib_rows_stance"}
+
+
+def calibration(workload):
+    """(read_factor, write_factor, source) measured on the workload's access pattern by the newest
+    committed calibration record (profiles/*/calib/calib_summary.json, tools/calib.sh), or None."""
+    import glob
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pat = next((v for k, v in CALIB_PATTERN.items() if workload.startswith(k)), None)
+    for f in sorted(glob.glob(os.path.join(root, "profiles", "*", "calib", "calib_summary.json")), reverse=True):
+        k = json.load(open(f))["kernels"].get(pat or "", {})
+        if "read_factor" in k and "write_factor" in k:
+            return k["read_factor"], k["write_factor"], os.path.relpath(f, root) + ":" + pat
+    return None
 
 
 def main():
@@ -56,11 +77,24 @@ def main():
     step_kernels = (sys.argv[5] if len(sys.argv) > 5 else "wbc_step_kernel").split(",")
     mean, n = summarise(pmc_dir)
     rec = {"workload": workload, "batch": batch, "dispatches": n, "per_launch": mean,
-           "kernel_source_sha256": kernel_source_hash(),
-           "traffic_note": ("HBM bytes per launch = FETCH_SIZE x 2 (gfx950: half of wide coalesced reads counted) "
+           "kernel_source_sha256": kernel_source_hash()}
+    cal = calibration(workload)
+    rf, wf = (cal[0], cal[1]) if cal else (2.0, 1.0)
+    rec["calibration"] = ({"read_factor": rf, "write_factor": wf, "source": cal[2]} if cal else None)
+    rec["traffic_note"] = (("HBM bytes per launch = FETCH_SIZE x %.3f + WRITE_SIZE x %.3f, KiB -> B: factors measured "
+                            "on this workload's own access pattern (%s); separate --pmc passes with --kernel-trace "
+                            "only" % (rf, wf, cal[2])) if cal else
+                           ("HBM bytes per launch = FETCH_SIZE x 2 (gfx950: half of wide coalesced reads counted) "
                             "+ WRITE_SIZE, KiB -> B; separate --pmc passes with --kernel-trace only; widths other "
-                            "than 16 B/lane are uncalibrated (MI355X_MICROARCH.md)")}
-    traffic = {k: traffic_bytes(m) for k, m in mean.items()}
+                            "than 16 B/lane are uncalibrated (MI355X_MICROARCH.md)"))
+    traffic = {k: traffic_bytes(m, rf, wf) for k, m in mean.items()}
+    rec["traffic_uncalibrated"] = {k: traffic_bytes(m) for k, m in mean.items()}
+    # executed fp64 VALU lane-operations per launch (an FMA counts 2), when the F64 counters ran
+    for k, m in mean.items():
+        if all(c in m for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64")):
+            rec.setdefault("fp64_executed_flops", {})[k] = 64.0 * (m["SQ_INSTS_VALU_ADD_F64"] + m["SQ_INSTS_VALU_MUL_F64"] +
+                                                                  2.0 * m["SQ_INSTS_VALU_FMA_F64"] +
+                                                                  m.get("SQ_INSTS_VALU_TRANS_F64", 0.0))
     # the step's kernels that ran (the default step runs one of them: wbc_update_solve_kernel, or
     # wbc_modes_kernel for mode hypotheses under the mode loop)
     ran = [k for k in step_kernels if traffic.get(k) is not None]

@@ -54,6 +54,13 @@ for tag, m in (("general", gen), ("stance", stn)):
         continue
     res[f"{tag}: solve setup (normals, slacks, J)"] = med(t11, st(15), m)
     res[f"{tag}: active-set loop"] = med(st(15), st(16), m)
+    res[f"{tag}:   hotstart block (warm re-adds, point, slacks)"] = med(st(15), st(25), m)
+    res[f"{tag}:   selection + loop passes"] = med(st(25), st(16), m)
+    # the loop's sub-steps summed over its passes (IST slots 0..5, lane 0 of the wave)
+    for i, n in enumerate(["normal row", "direction (d, R^-1 d, z)", "slack rates", "step lengths",
+                           "select + Householder add", "mirror (+ drop path)"]):
+        res[f"{tag}:   loop: {n}"] = float(np.median(D[m, i]))
+    res[f"{tag}:   loop: passes, drops (mean per wave)"] = [float(D[m, 6].mean()), float(D[m, 7].mean())]
     res[f"{tag}: primal + outputs"] = med(st(16), st(18), m)
     res[f"{tag}: total"] = med(st(0), st(18), m)
     res[f"{tag}: entry to end"] = med(st(30), st(18), m)
