@@ -52,7 +52,8 @@ def check_vs_oracle(out, rows, inp_rows):
     red = R.run_batch(inp_rows, method=R.REDUCED)
     assert np.array_equal(out["status"][rows], o["status"])
     same_it = out["iters"][rows] == red["iters"]
-    assert M.record("iters mismatch fraction", 1.0 - same_it.mean(), 0.01) <= 0.01, int((~same_it).sum())
+    # identical counts: near-ties are decided by one rule on both sides (WBC_TIE_BAND)
+    assert M.record("iters mismatch fraction", 1.0 - same_it.mean(), 0.0) == 0.0, int((~same_it).sum())
     ok = o["status"] == 0
     for j in np.nonzero(ok)[0]:
         b = rows[j]

@@ -16,12 +16,14 @@ Status, x and tau are the reference QP's whatever the form (checked against LITE
 choose the most violated row by slack / |row of the reference's A| and take the same partial /
 full steps, so they visit the same working sets:
 
-  * cold solves: identical status on every robot, identical `iters` on all but near-tie robots.
-    Ties are real in this QP: a foot at zero force has all four friction faces active at one
-    vertex, so several ratio-test candidates share u / r = 0 and rounding picks among them; the
-    two solvers then take routes of different length to the same optimum.  Allowed: 0.5 % of
-    robots on the RL batch, 5 % on the stress inputs (knees through straight, 6-80 N m limits);
-  * max_wsr lowered to 1, 2, 3: MAX_ITER exactly where the oracle hits it;
+  * cold solves: identical status and identical `iters` on every robot.  Ties are real in this QP
+    (the +-x faces of a foot with f_x = 0 are violated alike in exact arithmetic), and both sides
+    decide them by one rule: the lowest row id within WBC_TIE_BAND (1e-9 relative) of the most
+    violated row (include/wbc.h), so rounding no longer sends them down different
+    routes (round 4 allowed 0.5 % of robots on the RL batch and 5 % on the stress inputs).  The
+    split path's 24-variable form keeps a 1 % allowance on the stress inputs (4 of 512 robots at
+    6 N m differ, profiles/r05/parity_margins.json);
+  * max_wsr lowered: MAX_ITER exactly where the oracle hits it, on every robot;
   * stateful (hotstart from the previous working set, cpp:523-531): the oracle's Robot carries
     the same warm start, status and iterations agree step by step, also under a lowered cap.
 """
@@ -63,18 +65,19 @@ def engine_cold(inp, flags=0, **ov):
     return out
 
 
-CASES = {  # name: (inputs, params, min fraction of robots with identical iteration counts)
-    "rl_random": (lambda: workloads.rl_random(2048, 3), {}, 0.995),
-    "stress80": (lambda: stress_inputs(512, 51), dict(max_torque=80.0), 0.95),
-    "stress20": (lambda: stress_inputs(512, 52), dict(max_torque=20.0), 0.95),
-    "stress6": (lambda: stress_inputs(512, 53), dict(max_torque=6.0), 0.95),
+CASES = {  # name: (inputs, params, min fraction of robots with identical iteration counts: default, split)
+    "rl_random": (lambda: workloads.rl_random(2048, 3), {}, (1.0, 1.0)),
+    "stress80": (lambda: stress_inputs(512, 51), dict(max_torque=80.0), (1.0, 0.99)),
+    "stress20": (lambda: stress_inputs(512, 52), dict(max_torque=20.0), (1.0, 0.99)),
+    "stress6": (lambda: stress_inputs(512, 53), dict(max_torque=6.0), (1.0, 0.99)),
 }
 
 
 @pytest.mark.parametrize("path", sorted(PATHS))
 @pytest.mark.parametrize("case", sorted(CASES))
 def test_cold_iterations_match_oracle(case, path):
-    gen, ov, frac = CASES[case]
+    gen, ov, fracs = CASES[case]
+    frac = fracs[0] if path == "default" else fracs[1]
     flags, method = PATHS[path]
     inp = gen()
     g, o = engine_cold(inp, flags, **ov), R.run_batch(inp, method=method, **ov)
@@ -106,10 +109,9 @@ def test_max_iter_status_matches_oracle(case, max_wsr, path):
     hit = o["status"] == 1
     assert hit.any() and (~hit).any(), "cap must split the batch"
     mism = np.nonzero(g["status"] != o["status"])[0]
-    # a near-tie robot may take another route (see above); never more than 1 %
-    lim = max(1, len(inp["contacts"]) // 100)
-    assert M.record("MAX_ITER status mismatch fraction", len(mism) / len(inp["contacts"]),
-                    lim / len(inp["contacts"])) <= lim / len(inp["contacts"]), (case, max_wsr, mism[:10])
+    # both sides decide near-ties by the same rule (see above): the same robots hit the cap
+    assert M.record("MAX_ITER status mismatch fraction", len(mism) / len(inp["contacts"]), 0.0) == 0.0, \
+        (case, max_wsr, mism[:10])
     ok = (g["status"] == 0) & (o["status"] == 0)
     assert M.close(g["tau"][ok], o["tau"][ok], M.TAU, "tau")
     # MAX_ITER publishes nothing (the loop stops, cpp:654-659): zeros, iters = the cap
@@ -152,6 +154,6 @@ def test_hotstart_iterations_match_oracle(max_wsr, path):
                 assert M.close(g["tau"][b], o["tau"], M.TAU, "tau"), (t, b)
     e.close()
     assert n_it > 0
-    assert n_mism <= B * steps // 100, n_mism
+    assert M.record("status + iters mismatches per solve", n_mism / (B * steps), 0.002) <= 0.002, n_mism
     if max_wsr < 100:
         assert n_cap > 0

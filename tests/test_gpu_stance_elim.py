@@ -79,7 +79,7 @@ def test_inline_solve_equals_stance_kernel(maker, B):
     ker = run(inp, split=True)
     assert np.array_equal(inl["status"], ker["status"])
     assert M.record("iters mismatch fraction (inline vs stance kernel)",
-                    1.0 - (inl["iters"] == ker["iters"]).mean(), 0.005) <= 0.005
+                    1.0 - (inl["iters"] == ker["iters"]).mean(), 0.0) == 0.0
     assert (inl["status"] == 0).mean() > 0.9
     for k in ("tau", "grf", "x"):
         assert close(inl[k], ker[k], M.BITS, k), k
@@ -105,13 +105,13 @@ def test_stance_stress_inline_matches_oracle(max_torque, seed):
     o = R.run_batch(inp, max_torque=max_torque)
     assert np.array_equal(inl["status"], o["status"])
     assert np.array_equal(inl["status"], ker["status"])
-    # near-tie robots (a foot at zero force: several ratio-test candidates at u / r = 0) may take a
-    # route of different length to the same optimum under different rounding (test_gpu_iters.py)
-    # (stress inputs: many feet at zero force, so many near-ties; the solutions are checked below)
+    # near-ties (the +-x faces of a foot with f_x = 0, violated alike) are decided by one rule in the
+    # kernels and the oracle (WBC_TIE_BAND, test_gpu_iters.py): identical counts on every robot
+    # (round 4 allowed 10 % here)
     same_k, same_o = (inl["iters"] == ker["iters"]).mean(), (inl["iters"] == o["iters"]).mean()
-    M.record("iters mismatch fraction (inline vs stance kernel)", 1.0 - same_k, 0.10)
-    M.record("iters mismatch fraction (inline vs oracle)", 1.0 - same_o, 0.10)
-    assert same_k >= 0.90 and same_o >= 0.90, (same_k, same_o)
+    M.record("iters mismatch fraction (inline vs stance kernel)", 1.0 - same_k, 0.0)
+    M.record("iters mismatch fraction (inline vs oracle)", 1.0 - same_o, 0.0)
+    assert same_k == 1.0 and same_o == 1.0, (same_k, same_o)
     ok = o["status"] == 0
     assert ok.sum() > 0 and inl["iters"][ok].max() > 8
     if max_torque < 10.0:
