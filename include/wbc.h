@@ -118,6 +118,12 @@ enum {
                           * the stream before the step (one small kernel), as the engine does on the
                           * host for masks it copies.  Same results either way; it pays when the masks
                           * are mixed (waves of one mask), not when they are all equal (a trot). */
+#define WBC_RESIDENT 256u /* wbc_cycle only, B <= 4: the step stays resident on the GPU between cycles (one
+                          * workgroup polling a pinned mailbox), so a cycle costs no kernel launch and no
+                          * stream synchronisation (the B = 1 drop-in).  The resident wave
+                          * ends after 100 ms without a cycle, or at any other call on the engine (which
+                          * waits for it); the next WBC_RESIDENT cycle starts it again.  Same results as a
+                          * plain wbc_cycle. */
 
 /* Debug record layout (doubles per robot), written by update/step under WBC_DEBUG. */
 enum {

@@ -15,9 +15,9 @@ libwbc_controller.so), as the reference's class is.
 
 The product path has no CPU fallback: without libwbc_hip.so or a GPU it raises.
 """
-from ._capi import (COLD, DEBUG, FUSED, GROUP, NO_X, SPLIT, STATELESS, TIMED, QP_INFEASIBLE, QP_MAX_ITER, QP_NUMERIC, QP_OK, Engine, WbcError,  # noqa: F401
+from ._capi import (COLD, DEBUG, FUSED, GROUP, NO_X, RESIDENT, SPLIT, STATELESS, TIMED, QP_INFEASIBLE, QP_MAX_ITER, QP_NUMERIC, QP_OK, Engine, WbcError,  # noqa: F401
                     WbcModel, WbcParams, anymal_model, default_params, load_library, model_from_urdf, split_debug, Planner,
                     WbcPlannerParams)
 
 __all__ = ["Engine", "Planner", "WbcPlannerParams", "model_from_urdf", "WbcError", "WbcModel", "WbcParams", "anymal_model", "default_params", "load_library",
-           "split_debug", "STATELESS", "DEBUG", "NO_X", "SPLIT", "TIMED", "COLD", "FUSED", "GROUP", "QP_OK", "QP_MAX_ITER", "QP_INFEASIBLE", "QP_NUMERIC"]
+           "split_debug", "STATELESS", "DEBUG", "NO_X", "SPLIT", "TIMED", "COLD", "FUSED", "GROUP", "RESIDENT", "QP_OK", "QP_MAX_ITER", "QP_INFEASIBLE", "QP_NUMERIC"]

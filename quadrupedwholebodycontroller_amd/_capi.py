@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("WBC_LIB", os.path.join(HERE, "libwbc_hip.so"))
 
 NUM_JOINTS, NV, NC = 12, 42, 70
 POSE_LEN, NU_LEN, REF_LEN = 7, 18, 54
-STATELESS, DEBUG, NO_X, SPLIT, TIMED, COLD, FUSED, GROUP = 1, 2, 4, 8, 16, 32, 64, 128
+STATELESS, DEBUG, NO_X, SPLIT, TIMED, COLD, FUSED, GROUP, RESIDENT = 1, 2, 4, 8, 16, 32, 64, 128, 256
 QP_OK, QP_MAX_ITER, QP_INFEASIBLE, QP_NUMERIC = 0, 1, 2, 3
 
 # WBC_DBG_* offsets (include/wbc.h)

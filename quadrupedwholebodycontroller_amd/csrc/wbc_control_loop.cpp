@@ -222,10 +222,11 @@ int main(int argc, char** argv) {
             return run_stance(argc > 2 ? std::atol(argv[2]) : 1000, argc > 3 ? std::atof(argv[3]) : 0.0,
                               (argc > 4 && std::string(argv[4]) == "fused") ? WBC_FUSED
                               : (argc > 4 && std::string(argv[4]) == "split") ? WBC_SPLIT
-                              : 0u);  // "default" or nothing: the default step
+                              : (argc > 4 && std::string(argv[4]) == "launch") ? 0u  // a kernel launch per cycle
+                              : WBC_RESIDENT);  // "default" or nothing: the shim's default, the resident step
         if (mode == "replay" && argc > 3) return run_replay(argv[2], argv[3]);
         if (mode == "run") return run_node(argc > 2 ? std::atol(argv[2]) : 200);
-        std::fprintf(stderr, "usage: %s stance [cycles] [rate_hz] [fused|split|default] | run [cycles] | replay <in.bin> <out.bin>\n",
+        std::fprintf(stderr, "usage: %s stance [cycles] [rate_hz] [fused|split|launch|default] | run [cycles] | replay <in.bin> <out.bin>\n",
                      argv[0]);
         return 2;
     } catch (const std::exception& e) {

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -23,6 +24,10 @@ extern "C" hipError_t wbc_launch_update_solve(const wbc::KernelArgs* a, hipStrea
 extern "C" hipError_t wbc_launch_modes(const wbc::KernelArgs* a, hipStream_t st);
 extern "C" hipError_t wbc_launch_reset(double* hist, const uint8_t* mask, int batch, hipStream_t st);
 extern "C" hipError_t wbc_launch_qmap(const uint8_t* masks, int batch, int32_t* map, hipStream_t st);
+extern "C" hipError_t wbc_preload_resident();
+extern "C" hipError_t wbc_launch_resident(const wbc::KernelArgs* a, wbc::ResidentBox* box, const void* pin_in,
+                                          void* own_in, int in_words, unsigned long long seq0, unsigned long long idle_ticks,
+                                          hipStream_t st);
 
 namespace {
 thread_local std::string g_err;
@@ -119,6 +124,15 @@ struct wbc_engine {
     const void* m_in = nullptr;
     void* m_out = nullptr;
     const int32_t* m_qmap = nullptr;
+    // the resident control cycle (WBC_RESIDENT): mailbox (pinned, coherent), its stream, whether a
+    // resident wave runs and with which step flags, the last command posted, when it last answered
+    wbc::ResidentBox* res_box = nullptr;
+    wbc::ResidentBox* res_box_dev = nullptr;
+    hipStream_t res_stream = nullptr;
+    bool res_on = false;
+    uint32_t res_flags = 0;
+    unsigned long long res_seq = 0;
+    std::chrono::steady_clock::time_point res_last{};
 };
 
 namespace {
@@ -211,10 +225,42 @@ int64_t count_stance(const uint8_t* masks, size_t n) {
     return c;
 }
 
+// The resident cycle's mailbox (pinned, coherent) and stream; at wbc_create for B <= 4 (a few ms that
+// would otherwise land on the first resident cycle)
+hipError_t resident_alloc(wbc_engine* h) {
+    void* p = nullptr;
+    hipError_t e = hipHostMalloc(&p, sizeof(wbc::ResidentBox), hipHostMallocMapped | hipHostMallocCoherent);
+    if (e != hipSuccess) return e;
+    std::memset(p, 0, sizeof(wbc::ResidentBox));
+    h->res_box = static_cast<wbc::ResidentBox*>(p);
+    void* d = nullptr;
+    e = hipHostGetDevicePointer(&d, p, 0);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->res_stream, hipStreamNonBlocking);
+    h->res_box_dev = static_cast<wbc::ResidentBox*>(d);
+    h->res_seq = 0;
+    return e;
+}
+
+// The resident cycle's wave (WBC_RESIDENT) ends: WBC_RESIDENT_STOP posted, then its stream drained
+// (it may have ended by itself after its idle time: then the sync returns at once).
+hipError_t resident_stop(wbc_engine* h) {
+    if (!h->res_on) return hipSuccess;
+    h->res_on = false;
+    __atomic_store_n(&h->res_box->cmd, wbc::WBC_RESIDENT_STOP, __ATOMIC_RELEASE);
+    const hipError_t e = hipStreamSynchronize(h->res_stream);
+    __atomic_store_n(&h->res_box->cmd, h->res_seq, __ATOMIC_RELEASE);  // the next wave starts from res_seq
+    return e;
+}
+
 // After a zero-copy wbc_cycle the cycle's inputs, outputs and wave map live in the pinned blocks;
 // copy them into the engine's own device buffers, so every other call sees the state a copying
-// cycle leaves (synchronous: the pinned blocks are rewritten by the next cycle).
+// cycle leaves (synchronous: the pinned blocks are rewritten by the next cycle).  A resident cycle
+// wave is stopped first (every other call goes through here).
 hipError_t sync_own(wbc_engine* h) {
+    if (h->res_on) {
+        const hipError_t e = resident_stop(h);
+        if (e != hipSuccess) return e;
+    }
     if (!h->zc_stale) return hipSuccess;
     const size_t B = (size_t)h->batch;
     hipError_t e = hipSetDevice(h->device);
@@ -342,7 +388,9 @@ int32_t wbc_create(const wbc_model* model, const wbc_params* params, int32_t bat
     ALLOC(d_model, 1);
     ALLOC(d_params, 1);
     ALLOC(d_limg, wbc::LIMG_LEN);
-    if (hipMalloc(&h->d_inblk, in_block_bytes(B)) != hipSuccess || hipMalloc(&h->d_outblk, out_block_bytes(B)) != hipSuccess) {
+    // (the input block in whole 8-byte words: the resident cycle copies it by words)
+    if (hipMalloc(&h->d_inblk, (in_block_bytes(B) + 7) / 8 * 8) != hipSuccess ||
+        hipMalloc(&h->d_outblk, out_block_bytes(B)) != hipSuccess) {
         wbc_destroy(h);
         return fail(WBC_ERR_HIP, "hipMalloc failed: input/output blocks");
     }
@@ -374,6 +422,13 @@ int32_t wbc_create(const wbc_model* model, const wbc_params* params, int32_t bat
         return fail(WBC_ERR_HIP, "hipHostMalloc failed: wave map");
     }
     h->qmap_dev = h->d_qmap;
+    if (B <= (size_t)wbc::QMAP_SEG) {  // the resident cycle's code and mailbox, made ready now
+        (void)wbc_preload_resident();
+        if (resident_alloc(h) != hipSuccess) {
+            wbc_destroy(h);
+            return fail(WBC_ERR_HIP, "resident cycle mailbox / stream");
+        }
+    }
     if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) {
         wbc_destroy(h);
@@ -425,6 +480,9 @@ int32_t wbc_destroy(wbc_engine* h) {
     // drain the engine's in-flight work before freeing (the bound stream; never the whole device,
     // which would also wait for other engines' and the caller's unrelated work)
     (void)drain(h);
+    (void)resident_stop(h);
+    if (h->res_box) (void)hipHostFree(h->res_box);
+    if (h->res_stream) (void)hipStreamDestroy(h->res_stream);
     void* ptrs[] = {h->d_model, h->d_params, h->d_limg, h->d_inblk, h->d_outblk, h->d_mask, h->d_modes, h->d_hist, h->d_work,
                     h->d_fb, h->d_dbg, h->d_qmap};
     for (void* p : ptrs)
@@ -689,6 +747,60 @@ int32_t enqueue_cycle(wbc_engine* h, uint32_t flags) {
                                h->stream));
     return WBC_OK;
 }
+// The resident cycle (WBC_RESIDENT, B <= 4): start the wave if it is not running (or runs with other
+// flags, or may have ended by itself: no answer for 40 ms, against its 100 ms idle limit), post the
+// cycle, wait for its answer (bounded), and leave the outputs in the pinned output block.
+constexpr unsigned long long kResidentIdleTicks = 10000000ull;  // 100 ms of the 100 MHz constant clock
+constexpr auto kResidentRestart = std::chrono::milliseconds(40);
+constexpr auto kResidentAnswer = std::chrono::seconds(2);
+int32_t resident_cycle(wbc_engine* h, uint32_t flags) {
+    using clk = std::chrono::steady_clock;
+    const size_t B = (size_t)h->batch;
+    if (h->res_on && (h->res_flags != flags || clk::now() - h->res_last > kResidentRestart)) WBC_HIP(resident_stop(h));
+    if (!h->res_on) {
+        if (!h->res_box) WBC_HIP(resident_alloc(h));
+        // work queued on the engine stream (a reset, copies) completes before the wave reads the history
+        WBC_HIP(hipStreamSynchronize(h->stream));
+        // the step reads the engine's own device input block (the wave copies the pinned block into it
+        // every cycle) and writes the pinned output block through its device address
+        const double* ib = static_cast<const double*>(h->d_inblk);
+        double* ob = static_cast<double*>(h->m_out);
+        wbc::KernelArgs a = make_args(h, flags);
+        a.base_pose = ib;
+        a.nu = ib + B * WBC_POSE_LEN;
+        a.qj = a.nu + B * WBC_NU_LEN;
+        a.ref = a.qj + B * WBC_NUM_JOINTS;
+        a.contacts = reinterpret_cast<const uint8_t*>(a.ref + B * WBC_REF_LEN);
+        a.switching = a.contacts + B;
+        a.tau = ob;
+        a.grf = ob + B * WBC_NUM_JOINTS;
+        a.status = reinterpret_cast<int32_t*>(a.grf + B * WBC_NUM_JOINTS);
+        a.iters = a.status + B;
+        a.x = (flags & WBC_NO_X) ? nullptr : reinterpret_cast<double*>(a.iters + B);
+        a.elim = 1;  // as begin_step16: the default step
+        a.qmap = nullptr;  // one wave: its robots in batch order
+        a.nwaves = 1;
+        __atomic_store_n(&h->res_box->cmd, h->res_seq, __ATOMIC_RELEASE);
+        const int words = (int)((in_block_bytes(B) + 7) / 8);
+        WBC_HIP(wbc_launch_resident(&a, h->res_box_dev, h->m_in, h->d_inblk, words, h->res_seq, kResidentIdleTicks,
+                                    h->res_stream));
+        h->res_on = true;
+        h->res_flags = flags;
+    }
+    const unsigned long long seq = ++h->res_seq;
+    __atomic_store_n(&h->res_box->cmd, seq, __ATOMIC_RELEASE);  // the inputs (pinned) are written before
+    const auto deadline = clk::now() + kResidentAnswer;
+    while (__atomic_load_n(&h->res_box->done, __ATOMIC_ACQUIRE) != seq) {
+        if (clk::now() > deadline) {
+            (void)resident_stop(h);  // (the wave ends by itself within its idle limit)
+            return fail(WBC_ERR_HIP, "wbc_cycle: the resident step did not answer");
+        }
+        __builtin_ia32_pause();
+    }
+    h->res_last = clk::now();
+    h->zc_stale = true;  // the own buffers lag the pinned blocks until sync_own, as after a zero-copy cycle
+    return WBC_OK;
+}
 }  // namespace
 extern "C" {
 
@@ -702,7 +814,7 @@ int32_t wbc_cycle(wbc_engine* h, const double* base_pose, const double* nu, cons
     const size_t B = (size_t)h->batch;
     const size_t inb = in_block_bytes(B), outb = out_block_bytes(B);
     if (!h->h_in) {
-        WBC_HIP(hipHostMalloc(&h->h_in, inb, hipHostMallocMapped));
+        WBC_HIP(hipHostMalloc(&h->h_in, (inb + 7) / 8 * 8, hipHostMallocMapped));  // (whole words: the resident copy)
         WBC_HIP(hipHostMalloc(&h->h_out, outb, hipHostMallocMapped));
 #ifndef WBC_CYCLE_COPY  // (A/B builds only: the copy cycle at every batch size)
         // Small batches (the B = 1 drop-in) run zero-copy: the step reads the pinned input block and
@@ -739,12 +851,16 @@ int32_t wbc_cycle(wbc_engine* h, const double* base_pose, const double* nu, cons
     h->qmap_waves = wbc::qmap_build(contacts, h->batch, h->h_qmap);  // uploaded by enqueue_cycle
     h->qmap_host = true;
     if (!x) flags |= WBC_NO_X;
-    {
-        const int32_t rc = enqueue_cycle(h, flags);
+    if ((flags & WBC_RESIDENT) && h->m_in && B <= (size_t)wbc::QMAP_SEG && !(flags & (WBC_SPLIT | WBC_FUSED | WBC_DEBUG))) {
+        const int32_t rc = resident_cycle(h, flags & ~WBC_RESIDENT);
         if (rc != WBC_OK) return rc;
+    } else {
+        if (h->res_on) WBC_HIP(resident_stop(h));
+        const int32_t rc = enqueue_cycle(h, flags & ~WBC_RESIDENT);
+        if (rc != WBC_OK) return rc;
+        WBC_HIP(hipStreamSynchronize(h->stream));
     }
     const size_t xb = B * WBC_NV * sizeof(double);
-    WBC_HIP(hipStreamSynchronize(h->stream));
     const double* o = static_cast<const double*>(h->h_out);
     if (tau) std::memcpy(tau, o, B * WBC_NUM_JOINTS * sizeof(double));
     if (grf) std::memcpy(grf, o + B * WBC_NUM_JOINTS, B * WBC_NUM_JOINTS * sizeof(double));

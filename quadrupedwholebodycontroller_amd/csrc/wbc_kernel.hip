@@ -2314,7 +2314,7 @@ __device__ __forceinline__ void leg_bounds(double kr1, double ksw, double ko, do
 }
 
 template <int SUB, bool SOLVE = false, typename Model = wbc_model, bool MLOOP = false, int STF = -1>
-__device__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int lane, bool wr, UpdScratch& s, Prob& P,
+__device__ __forceinline__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int lane, bool wr, UpdScratch& s, Prob& P,
                              Presolve* pre, const Model& md, const double* fric = nullptr,
                              const double* vin = nullptr, int chunk = 0, unsigned* fails = nullptr) {
     const wbc_params& pr = a.pv;
@@ -4591,6 +4591,91 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) {
                            reinterpret_cast<SolveLds*>(&L));
 }
 
+// The resident control cycle (wbc_cycle with WBC_RESIDENT, B <= 4: one wave): the step above,
+// looped in one workgroup that stays on the GPU between control cycles, so a cycle costs no kernel
+// launch and no stream synchronisation.  The host packs the cycle's inputs into
+// the pinned input block, then raises box->cmd; the wave polls it (one lane, relaxed system-scope
+// atomic loads, which bypass the caches, s_sleep between polls), copies the pinned input block
+// into the engine's own device input block with the same loads (no acquire fence: a system-scope
+// acquire invalidates the L2 and, polled, left the step's code and model to be fetched from HBM
+// again every cycle), runs the step on it, writing the outputs to the pinned output block, and
+// publishes box->done = cmd after a system-scope release of those stores.  Every wave of the loop
+// ends: on WBC_RESIDENT_STOP, or when no command arrives within idle_ticks of the 100 MHz constant
+// clock (s_memrealtime), so a host that stops posting (or exits) never leaves the wave spinning;
+// the host relaunches it after any pause of half that time.
+template <int STF>
+WBC_UPDATE_KERNEL_ATTR void wbc_resident_kernel(KernelArgs a, ResidentBox* box, const unsigned long long* pin_in,
+                                                unsigned long long* own_in, int in_words, unsigned long long seq0,
+                                                unsigned long long idle_ticks) {
+    __shared__ UpdLds L;
+    __shared__ unsigned long long cmd_s;
+    const int seg = (int)threadIdx.x / UPD_SUB, lane = (int)threadIdx.x % UPD_SUB;
+    unsigned long long last = seq0;
+    for (;;) {
+        if (threadIdx.x == 0) {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            unsigned long long c;
+            for (;;) {
+                c = __hip_atomic_load(&box->cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (c != last) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) { c = WBC_RESIDENT_STOP; break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            cmd_s = c;
+        }
+        __syncthreads();
+        const unsigned long long cmd = cmd_s;
+        __syncthreads();
+        if (cmd == WBC_RESIDENT_STOP) break;
+        // the cycle's inputs: the pinned block's words (loads in one batch: two per lane covers B <= 1,
+        // the loop the rest) into the engine's device block, which update_phase reads (KernelArgs'
+        // input pointers point there)
+        {
+            const int t = (int)threadIdx.x;
+            const int k0 = t < in_words ? t : in_words - 1, k1 = t + 64 < in_words ? t + 64 : in_words - 1;
+            const unsigned long long w0 = __hip_atomic_load(&pin_in[k0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            const unsigned long long w1 = __hip_atomic_load(&pin_in[k1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            own_in[k0] = w0;
+            own_in[k1] = w1;
+            for (int k = t + 128; k < in_words; k += 64)
+                own_in[k] = __hip_atomic_load(&pin_in[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        __syncthreads();
+        const int e = seg;
+        const bool wr = e < a.batch;
+        const int qp = wr ? e : a.batch - 1, row = qp;
+        const int kap = a.contacts[row] & 15;
+        double vin[(91 + UPD_SUB - 1) / UPD_SUB];
+        load_inputs<UPD_SUB>(a, row, lane, vin);
+        stage_to_lds<LIMG_LEN>(reinterpret_cast<double*>(&L), a.limg, (int)threadIdx.x);
+        lds_sync();
+        const bool solved = update_phase<UPD_SUB, true, LdsModel, false, STF>(a, row, qp, kap, lane, wr, L.u[seg], L.prob[seg],
+                                                                            nullptr, L.model, &L.fric[0], vin);
+        const bool fb = wr && !solved;
+        if (fb) {
+            const double2* src = reinterpret_cast<const double2*>(&L.prob[seg]);
+            double* wrow = a.work + (size_t)qp * WORK_LEN;
+            double2* dst = reinterpret_cast<double2*>(wrow);
+            for (int k = lane; k < PROB_LEN / 2; k += UPD_SUB) dst[k] = src[k];
+            if (lane == 0) {
+                Presolve* pre = reinterpret_cast<Presolve*>(wrow + PROB_LEN);
+                pre->presolved = 0.0;
+                pre->stance = 0.0;
+            }
+        }
+        const unsigned long long fm = __ballot(fb && lane == 0);
+        if (fm)
+            drain_fallbacks<4 + STF>((const KernelArgs*)__builtin_amdgcn_kernarg_segment_ptr(), fm, qp,
+                                     reinterpret_cast<SolveLds*>(&L));
+        // outputs (pinned host memory) and history (HBM) stored, then the cycle published
+        __syncthreads();
+        __threadfence_system();
+        if (threadIdx.x == 0) __hip_atomic_store(&box->done, cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        last = cmd;
+        __syncthreads();
+    }
+}
+
 // Mode hypotheses with the update shared (KernelArgs::mloop = M > 1): workgroup g C + c (C = K / M
 // chunks, xcd_block order, so a state group's chunks share an L2) runs states 4 g .. 4 g + 3, each
 // segment through one update and then the M hypotheses of chunk c (update_phase's mode loop);
@@ -4929,6 +5014,29 @@ extern "C" hipError_t wbc_launch_update_solve(const wbc::KernelArgs* a, hipStrea
     else
         hipLaunchKernelGGL(wbc::wbc_update_solve_kernel<0>, dim3(a->nwaves), dim3(64), 0, st, *a);
     return hipGetLastError();
+}
+// The resident control cycle (one workgroup, B <= 4), until WBC_RESIDENT_STOP or idle_ticks without a command
+extern "C" hipError_t wbc_launch_resident(const wbc::KernelArgs* a, wbc::ResidentBox* box, const void* pin_in,
+                                          void* own_in, int in_words, unsigned long long seq0, unsigned long long idle_ticks,
+                                          hipStream_t st) {
+    // B <= 4: the 2 B mask bytes fit the one word after the 91 B doubles
+    if (a->batch <= 0 || a->batch > wbc::UPD_RPW || a->qmap || a->modes || in_words != 91 * a->batch + 1)
+        return hipErrorInvalidValue;
+    const auto* pin = static_cast<const unsigned long long*>(pin_in);
+    auto* own = static_cast<unsigned long long*>(own_in);
+    if (a->stateful)
+        hipLaunchKernelGGL(wbc::wbc_resident_kernel<1>, dim3(1), dim3(64), 0, st, *a, box, pin, own, in_words, seq0, idle_ticks);
+    else
+        hipLaunchKernelGGL(wbc::wbc_resident_kernel<0>, dim3(1), dim3(64), 0, st, *a, box, pin, own, in_words, seq0, idle_ticks);
+    return hipGetLastError();
+}
+// Loads the resident kernels' code now (small engines: the B = 1 drop-in), so that the first resident
+// cycle does not pay the code object's lazy load (~10 ms, which showed in the control loop's mean)
+extern "C" hipError_t wbc_preload_resident() {
+    hipFuncAttributes at;
+    hipError_t e = hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&wbc::wbc_resident_kernel<1>));
+    if (e == hipSuccess) e = hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&wbc::wbc_resident_kernel<0>));
+    return e;
 }
 extern "C" hipError_t wbc_launch_reset(double* hist, const uint8_t* mask, int batch, hipStream_t st) {
     hipLaunchKernelGGL(wbc::wbc_reset_kernel, dim3(batch), dim3(64), 0, st, hist, mask, batch);

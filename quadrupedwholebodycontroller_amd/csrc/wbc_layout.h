@@ -117,6 +117,17 @@ inline void build_lds_image(const wbc_model& m, double friction, LdsImage& o) {
     }
 }
 
+// The resident control cycle's mailbox (wbc_cycle with WBC_RESIDENT; pinned, coherent host memory):
+// the host raises cmd (a sequence number, or WBC_RESIDENT_STOP), the resident wave answers with
+// done = cmd once the cycle's outputs are visible.  The two words sit on separate 64-byte lines.
+constexpr unsigned long long WBC_RESIDENT_STOP = ~0ull;
+struct ResidentBox {
+    unsigned long long cmd;
+    unsigned long long pad0[7];
+    unsigned long long done;
+    unsigned long long pad1[7];
+};
+
 // Kernel arguments (one struct, passed by value).
 struct KernelArgs {
     const wbc_model* model;

@@ -5,7 +5,7 @@ without x, and leave caller-bound output buffers bound."""
 import numpy as np
 import pytest
 
-from quadrupedwholebodycontroller_amd import STATELESS, Engine, WbcError, workloads
+from quadrupedwholebodycontroller_amd import RESIDENT, STATELESS, Engine, WbcError, workloads
 
 pytestmark = pytest.mark.gpu
 
@@ -133,3 +133,49 @@ def test_zero_copy_cycle_then_plain_step_mixed_masks(B):
             assert np.array_equal(got[k], want[k]), (flags, k)
             assert np.array_equal(after[k], want[k]), (flags, k)
             assert np.array_equal(got2[k], want2[k]), (flags, k)
+
+
+@pytest.mark.parametrize("B", [1, 4])
+def test_resident_cycle_equals_separate_calls(B):
+    """WBC_RESIDENT (B <= 4): the step stays on the GPU between cycles, polling a pinned mailbox
+    (DESIGN.md 4.18).  A stateful trot, every cycle equal to the separate calls, with the resident
+    wave stopped and restarted on the way: by a plain wbc_step / wbc_get_output (any other call
+    stops it), by a change of flags (x on / off), and by a pause longer than the host's restart
+    limit (the wave may have ended by its idle limit)."""
+    import time
+
+    seq = list(workloads.trot_sequence(B, steps=40, seed=11))
+    e1, e2 = Engine(B), Engine(B)
+    for t, s in enumerate(seq):
+        want = separate_calls(e1, s, 0)
+        got = e2.cycle(s["base_pose"], s["nu"], s["qj"], s["ref"], s["contacts"], s["switching"], RESIDENT,
+                       want_x=(t % 10 < 7))
+        for k in ("tau", "grf", "status", "iters"):
+            assert np.array_equal(got[k], want[k]), (t, k)
+        if t % 10 < 7:
+            assert np.array_equal(got["x"], want["x"]), t
+        if t == 15:  # any other call stops the resident wave and sees the cycle's state
+            o = e2.outputs()
+            for k in ("tau", "grf", "status", "iters"):
+                assert np.array_equal(o[k], want[k]), (t, k)
+        if t == 25:
+            time.sleep(0.15)  # longer than the wave's idle limit: it has ended; the next cycle restarts it
+    e1.close()
+    e2.close()
+
+
+def test_resident_cycle_then_plain_steps():
+    """After resident cycles, plain steps on the engine's own buffers continue the same history."""
+    B = 1
+    seq = list(workloads.trot_sequence(B, steps=20, seed=12))
+    e1, e2 = Engine(B), Engine(B)
+    for t, s in enumerate(seq):
+        want = separate_calls(e1, s, 0)
+        if t < 10:
+            got = e2.cycle(s["base_pose"], s["nu"], s["qj"], s["ref"], s["contacts"], s["switching"], RESIDENT)
+        else:
+            got = separate_calls(e2, s, 0)
+        for k in KEYS:
+            assert np.array_equal(got[k], want[k]), (t, k)
+    e1.close()
+    e2.close()

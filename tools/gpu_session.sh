@@ -33,6 +33,10 @@ PY
            WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_istamps.so timeout -k 10 200 python tools/ust16.py $c $B > $O/ust_$c.log 2>&1; rc=$?
            [ $rc -ne 0 ] && break
          done; grep -h "loop\|hotstart\|entry to end" $O/ust_*.log | head -40 ;;
+    b1) for m in default launch default launch; do
+          timeout -k 10 120 quadrupedwholebodycontroller_amd/wbc_control_loop stance 3000 0 $m >> $O/b1_$m.log 2>&1; rc=$?
+          [ $rc -ne 0 ] && break
+        done; tail -n 2 $O/b1_default.log $O/b1_launch.log | cut -c1-200 ;;
     listc) timeout -k 10 120 rocprofv3 -L > $O/counters.txt 2>&1; rc=$?; grep -o "SQ_INSTS_VALU[A-Z0-9_]*F64[A-Z0-9_]*" $O/counters.txt | sort -u ;;
     pmc) CONFIG=${PMC_CONFIG:-stance_cold_b4096} BATCH=${PMC_BATCH:-4096} TAG=${TAG}_$PMC_CONFIG bash tools/pmc.sh > $O/pmc_$PMC_CONFIG.log 2>&1; rc=$?; tail -3 $O/pmc_$PMC_CONFIG.log ;;
     *) echo "unknown step $s"; rc=2 ;;
