@@ -150,9 +150,9 @@ def _cpu_baseline_numpy(inp, budget_s):
                 sample=f"{n} cold solves through oracle/wbc_np.py (numpy restatement), 1 thread, {dt:.2f} s")
 
 
-def committed_traffic(workload, batch):
-    """HBM bytes per launch, per kernel and per step, from a committed PMC summary
-    (tools/pmc_summary.py) taken on this exact kernel source, workload and batch; {} if none."""
+def committed_pmc(workload, batch):
+    """The committed PMC summary (tools/pmc_summary.py) taken on this exact kernel source, workload and
+    batch, and its path; (None, None) if none."""
     import glob
 
     sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -166,8 +166,28 @@ def committed_traffic(workload, batch):
             continue
         if (rec.get("kernel_source_sha256") == want and rec.get("workload") == workload and
                 rec.get("batch") == batch and "traffic" in rec):
-            return rec["traffic"], os.path.relpath(f, ROOT)
-    return {}, None
+            return rec, os.path.relpath(f, ROOT)
+    return None, None
+
+
+def committed_traffic(workload, batch):
+    """HBM bytes per launch, per kernel and per step, from the committed PMC summary; {} if none."""
+    rec, src = committed_pmc(workload, batch)
+    return (rec["traffic"], src) if rec else ({}, None)
+
+
+def executed_fp64(workload, batch, kernel, kernel_ms):
+    """The fp64 VALU work the kernel actually issued (SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 x 64 lanes, an
+    FMA counted twice, every lane of an issued instruction counted) per launch, from the committed PMC
+    summary, over this run's kernel time: TFLOP/s and the fraction of the fp64 peak; None without it."""
+    rec, src = committed_pmc(workload, batch)
+    f = (rec or {}).get("fp64_executed_flops", {}).get(kernel)
+    if not f:
+        return None
+    tf = f / (kernel_ms * 1e-3) / 1e12
+    return {"flops_per_launch": f, "achieved": tf, "frac": tf / FP64_PEAK_TFLOPS, "source": src,
+            "note": "issued fp64 VALU lane-operations (64 lanes per instruction, masked lanes included) from the "
+                    "PMC counters, beside the reference-equivalent flops of SURVEY 8(d) used for frac"}
 
 
 def step_flops(S, iters):
@@ -249,6 +269,7 @@ def bench_trot(torch, stream, device, STATELESS, B=4096, T=400, seed=2):
     rl = roofline_of(step_flops(B * T, its) / T, ms / T, tr.get("step"), tr_src)
     rl["note"] = "per step (one wbc_update_solve_kernel launch): flops of the 400-step " \
                  "sequence / 400 over the sequence's HIP-event time / 400"
+    rl["executed_fp64"] = executed_fp64("trot_stateful_b4096", B, "wbc_update_solve_kernel", ms / T)
     step_s = ms / T * 1e-3
     hbm = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "achieved": B * BYTES_TROT_ENGINE / step_s / 1e9,
@@ -474,9 +495,11 @@ def main():
                                                     step_kernel(e2)),
                                traffic_per_step=tr2.get("step"), traffic_source=tr2_src,
                                algorithmic_bytes_per_step=float(S2 * BYTES_IN + B2 * BYTES_OUT))
+            extra[name]["roofline"]["executed_fp64"] = executed_fp64(name, B2, step_kernel(e2), ms2)
             e2.close()
 
     traffic, traffic_src = committed_traffic(args.config, B)
+    pmc_rec, _ = committed_pmc(args.config, B)
     total = (B * world if scaling == "weak" else B_total) * args.steps
     value = total / elapsed
     result = {
@@ -506,7 +529,9 @@ def main():
                              "vector peak); SURVEY 8(d) algorithmic flops: F_dyn + F_asm per state, F_fact + F_tau + "
                              "k F_iter per QP, k = iters[] (working-set changes of the 12-variable form the engine "
                              "solves); latency/issue-bound small dense linear algebra",
-                     "flops_per_launch": flops_step},
+                     "flops_per_launch": flops_step,
+                     "traffic_calibration": (pmc_rec or {}).get("calibration"),
+                     "executed_fp64": executed_fp64(args.config, B, dom, dom_ms)},
         "roofline_hbm": {"bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": hbm_gbs / HBM_PEAK_GBS, "bytes_per_solve": bytes_step / B,
                          "traffic": sum(traffic.get(k, 0) for k in kernels) if traffic else None,

@@ -4604,50 +4604,74 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) {
 // clock (s_memrealtime), so a host that stops posting (or exits) never leaves the wave spinning;
 // the host relaunches it after any pause of half that time.
 template <int STF>
-WBC_UPDATE_KERNEL_ATTR void wbc_resident_kernel(KernelArgs a, ResidentBox* box, const unsigned long long* pin_in,
+WBC_UPDATE_KERNEL_ATTR void wbc_resident_kernel(KernelArgs args, ResidentBox* box, const unsigned long long* pin_in,
                                                 unsigned long long* own_in, int in_words, unsigned long long seq0,
                                                 unsigned long long idle_ticks) {
     __shared__ UpdLds L;
-    __shared__ unsigned long long cmd_s;
-    const int seg = (int)threadIdx.x / UPD_SUB, lane = (int)threadIdx.x % UPD_SUB;
-    unsigned long long last = seq0;
+    // the loop's own state lives in LDS, re-read after every barrier: kept in registers across the
+    // step body it was spilled to scratch (the body needs every register it has)
+    __shared__ struct {
+        ResidentBox* box;
+        const unsigned long long* pin;
+        unsigned long long *own, last, idle, cmd;
+        int words;
+    } C;
+    (void)args;
+    if (threadIdx.x == 0) {
+        C.box = box;
+        C.pin = pin_in;
+        C.own = own_in;
+        C.last = seq0;
+        C.idle = idle_ticks;
+        C.words = in_words;
+    }
     for (;;) {
+        __syncthreads();
         if (threadIdx.x == 0) {
+            ResidentBox* bx = C.box;
+            const unsigned long long last = C.last, idle = C.idle;
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
             unsigned long long c;
             for (;;) {
-                c = __hip_atomic_load(&box->cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                c = __hip_atomic_load(&bx->cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (c != last) break;
-                if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) { c = WBC_RESIDENT_STOP; break; }
+                if (__builtin_amdgcn_s_memrealtime() - t0 > idle) { c = WBC_RESIDENT_STOP; break; }
                 __builtin_amdgcn_s_sleep(1);
             }
-            cmd_s = c;
+            C.cmd = c;
         }
         __syncthreads();
-        const unsigned long long cmd = cmd_s;
-        __syncthreads();
-        if (cmd == WBC_RESIDENT_STOP) break;
+        if (C.cmd == WBC_RESIDENT_STOP) break;
         // the cycle's inputs: the pinned block's words (loads in one batch: two per lane covers B <= 1,
         // the loop the rest) into the engine's device block, which update_phase reads (KernelArgs'
         // input pointers point there)
         {
-            const int t = (int)threadIdx.x;
-            const int k0 = t < in_words ? t : in_words - 1, k1 = t + 64 < in_words ? t + 64 : in_words - 1;
-            const unsigned long long w0 = __hip_atomic_load(&pin_in[k0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            const unsigned long long w1 = __hip_atomic_load(&pin_in[k1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            own_in[k0] = w0;
-            own_in[k1] = w1;
-            for (int k = t + 128; k < in_words; k += 64)
-                own_in[k] = __hip_atomic_load(&pin_in[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            const unsigned long long* pin = C.pin;
+            unsigned long long* own = C.own;
+            const int t = (int)threadIdx.x, nw = C.words;
+            const int k0 = t < nw ? t : nw - 1, k1 = t + 64 < nw ? t + 64 : nw - 1;
+            const unsigned long long w0 = __hip_atomic_load(&pin[k0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            const unsigned long long w1 = __hip_atomic_load(&pin[k1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            own[k0] = w0;
+            own[k1] = w1;
+            for (int k = t + 128; k < nw; k += 64)
+                own[k] = __hip_atomic_load(&pin[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         __syncthreads();
+        // the step's arguments and lane ids are re-derived every cycle through an opaque copy: loop-
+        // invariant, the compiler hoisted their derived values out of the loop and spilled them
+        const KernelArgs* ap = (const KernelArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+        int tid = (int)threadIdx.x;
+        asm volatile("" : "+s"(ap), "+v"(tid));
+        const KernelArgs& a = *ap;
+        const int seg = tid / UPD_SUB, lane = tid % UPD_SUB;
         const int e = seg;
         const bool wr = e < a.batch;
         const int qp = wr ? e : a.batch - 1, row = qp;
         const int kap = a.contacts[row] & 15;
         double vin[(91 + UPD_SUB - 1) / UPD_SUB];
         load_inputs<UPD_SUB>(a, row, lane, vin);
-        stage_to_lds<LIMG_LEN>(reinterpret_cast<double*>(&L), a.limg, (int)threadIdx.x);
+        stage_to_lds<LIMG_LEN>(reinterpret_cast<double*>(&L), a.limg, tid);
         lds_sync();
         const bool solved = update_phase<UPD_SUB, true, LdsModel, false, STF>(a, row, qp, kap, lane, wr, L.u[seg], L.prob[seg],
                                                                             nullptr, L.model, &L.fric[0], vin);
@@ -4665,14 +4689,16 @@ WBC_UPDATE_KERNEL_ATTR void wbc_resident_kernel(KernelArgs a, ResidentBox* box, 
         }
         const unsigned long long fm = __ballot(fb && lane == 0);
         if (fm)
-            drain_fallbacks<4 + STF>((const KernelArgs*)__builtin_amdgcn_kernarg_segment_ptr(), fm, qp,
+            drain_fallbacks<4 + STF>(ap, fm, qp,
                                      reinterpret_cast<SolveLds*>(&L));
         // outputs (pinned host memory) and history (HBM) stored, then the cycle published
         __syncthreads();
         __threadfence_system();
-        if (threadIdx.x == 0) __hip_atomic_store(&box->done, cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        last = cmd;
-        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned long long cmd = C.cmd;
+            __hip_atomic_store(&C.box->done, cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            C.last = cmd;
+        }
     }
 }
 

@@ -15,8 +15,10 @@ def test_step_kernels_scratch_free():
     """Every kernel's own code is free of scratch (spill) instructions.  Exceptions, the rare paths:
     the fallback kernel (its list loop keeps the arguments live through the solve) and
     drain_fallbacks, the call in which the default step's wave (and the mode loop's,
-    wbc_modes_kernel) solves its own fallbacks (only the callee touches the stack; the kernel body
-    stays scratch-free)."""
+    wbc_modes_kernel, and the resident control cycle's, wbc_resident_kernel) solves its own
+    fallbacks (only the callee touches the stack; the kernel body stays scratch-free).  The
+    resident kernel's loop keeps its state in LDS and re-derives the arguments every cycle: held in
+    registers across the step body they were spilled (309 scratch instructions)."""
     mk = open(os.path.join(CSRC, "Makefile")).read()
     waves = re.search(r"^WAVES \?= (\d+)", mk, re.M).group(1)
     kflags = re.search(r"^KFLAGS := (.*)$", mk, re.M).group(1).split()  # the kernel's own flags
@@ -37,7 +39,8 @@ def test_step_kernels_scratch_free():
         spill = [l for l in body if "scratch_" in l]
         assert not spill, (n, spill[:3])
         calls = [l for l in body if "s_swappc" in l]
-        assert not calls or "update_solve" in n or "modes_kernel" in n, (n, calls)
+        assert not calls or "update_solve" in n or "modes_kernel" in n or "resident_kernel" in n, (n, calls)
     assert any("solve_stance" in n for n in names)
     assert any("update_solve" in n for n in names) and any("drain_fallbacks" in n for n in names)
     assert any("modes_kernel" in n for n in names)
+    assert sum("resident_kernel" in n for n in names) == 2

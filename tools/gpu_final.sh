@@ -5,10 +5,12 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 TAG=${TAG:-final}
-ROUND=${ROUND:-r04}
+ROUND=${ROUND:-r05}
 O=gpurun_out/$TAG
 mkdir -p $O profiles/$ROUND
 step() { local name=$1 t=$2; shift 2; echo "== $name $(date +%T)"; timeout -k 10 $t "$@" > $O/$name.log 2>&1; local rc=$?; echo "== $name rc=$rc"; if [ $rc -ne 0 ]; then tail -30 $O/$name.log; exit $rc; fi; }
+step calib 300 env OUT=$O/calib bash tools/calib.sh
+mkdir -p profiles/$ROUND/calib && cp $O/calib/calib_summary.json $O/calib/known.json $O/calib/pass*_counter_collection.csv profiles/$ROUND/calib/
 step pytest 400 env WBC_MARGINS_OUT=$O/parity_margins.json python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
 cp $O/parity_margins.json profiles/$ROUND/parity_margins.json
 step smoke 120 python -c "import __graft_entry__ as g; g.smoke()"
@@ -25,7 +27,9 @@ for cb in rl_random_b8192 modes16_b16384; do
   step prof_$cb 300 rocprofv3 --kernel-trace --stats -d $O/prof_$cb -o prof --output-format csv -- python3 bench.py --config $cb --steps 50 --warmup 5 --no-cpu-baseline
 done
 step b1_fused 120 quadrupedwholebodycontroller_amd/wbc_control_loop stance 3000 0 fused
+step b1_launch 120 quadrupedwholebodycontroller_amd/wbc_control_loop stance 3000 0 launch
 step b1_default 120 quadrupedwholebodycontroller_amd/wbc_control_loop stance 3000 0 default
+step qmap_probe 200 python tools/qmap_probe.py 30
 step b1_probe 120 python tools/b1_probe.py 2000
 step batch_sweep 180 python tools/batch_sweep.py 50
 step ust_stance 120 env WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_istamps.so python tools/ust16.py stance_cold 4096
