@@ -198,9 +198,9 @@ private:
     int footContacts_[numberOfLegs] = {1, 1, 1, 1};
     bool isSwitchingFootState_ = false;
 
-    // one robot: the default step (one launch, the 12-variable form with its hotstart) measured
-    // 41.2 us per cycle against 44.5 us for WBC_FUSED (one robot per wave, the 24-variable form;
-    // profiles/r03/c/b1_default.log, b1_fused.log)
+    // one robot, per control cycle (profiles/r05/b1_*.log, mean / p99): the resident step
+    // (WBC_RESIDENT) 27.4 / 27.5 us, a launch per cycle (0) 34.5 / 39.2 us, WBC_FUSED (one robot
+    // per wave, the 24-variable form) 38.1 / 42.6 us
     uint32_t stepFlags_ = WBC_RESIDENT;
     int qpStatus_ = WBC_QP_OK;
     int qpIters_ = 0;

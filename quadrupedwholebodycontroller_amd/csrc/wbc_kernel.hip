@@ -1,8 +1,13 @@
 // wbc_kernel.hip — batched whole-body-control step for gfx950 (MI355X), fp64.
 //
-// One robot per 64-lane wavefront (one workgroup = one wave).  Default occupancy: 2 waves per
-// SIMD (<= 256 VGPRs, spill-free; 8 robots per CU, ~9.6 KB of LDS per robot); the 4-wave build
-// (<= 128 VGPRs) spills and is slower (profiles/r01/variants_*.log).
+// The default step (wbc_update_solve_kernel, the mode loop wbc_modes_kernel and the resident B <= 4
+// cycle wbc_resident_kernel) runs four robots per 64-lane wavefront, a 16-lane segment each, one
+// workgroup = one wave, one wave per SIMD (≈ 400 registers, 40 KB of LDS), and solves each robot's
+// QP in its exact 12-variable reduction (DESIGN.md 4.8, 4.4/4.6 for the stateless stance form).
+// The split and fused forms (wbc_update_kernel + wbc_solve_kernel, wbc_step_kernel) run the
+// 24-variable general QP described below one robot per wave at WBC_WAVES_PER_SIMD = 2 (<= 256
+// VGPRs, spill-free, 20.3 KB of LDS); their 4-wave build spills and is slower
+// (profiles/r01/variants_*.log).
 //
 //   update (≙ WholeBodyController::updateState, src/whole_body_controller.cpp:256-294)
 //     stage A  lanes 0..11 = joints: sin/cos; lanes 0..3 = legs: forward kinematics chain
@@ -13,8 +18,8 @@
 //              closed forms of T^-1, Mbar = T^-T M T^-1, Jbar = J T^-1, bbar (cpp:268-293) instead
 //              of the reference's seven dense 18x18 LU inverses; finite differences against the
 //              HBM history (cpp:384-402); desired wrench and swing commands (cpp:426-464).
-//   solve (≙ solveQP + computeJointTorques, cpp:466-577)
-//     The 42-variable / 70-row QP is reduced exactly to 24 variables (DESIGN.md §QP) and solved
+//   solve (≙ solveQP + computeJointTorques, cpp:466-577), split and fused forms
+//     The 42-variable / 70-row QP is reduced exactly to 24 variables (DESIGN.md 4.2) and solved
 //     with the Goldfarb-Idnani dual active-set method: lane p owns constraint p and its column
 //     C[:,p] = J^T n_p (J = L^-T Q), so every product the method needs is lane-local; the chosen
 //     column is broadcast with v_readlane; R^-1 (packed) lives in LDS; Householder reflections

@@ -1,7 +1,7 @@
 """GPU parity: the HIP engine (through the C-ABI) against the numpy oracle of the reference path.
 
-Tolerances (fp64 everywhere; tests/margins.py, tightened in round 4 to 10-80x the worst error
-measured on MI355X, profiles/r04/parity_margins.json, well inside BASELINE.md's parity gate):
+Tolerances (fp64 everywhere; tests/margins.py, tightened in round 4; 6-53x the worst error
+measured on MI355X in round 5, profiles/r05/parity_margins.json, well inside BASELINE.md's parity gate):
   intermediates (M, C nu, Jacobians, CoM, Mbar, Jbar, bbar, wrench, bounds): 1e-13 relative to
     max(1, |value|) (W 5e-12, Mbar_b and rsw 1e-12; the kinematics, Jbar and Mbar_j 1e-14) -- the kernel uses closed forms instead of the
     reference's dense LU inverses, so agreement is to rounding, not bitwise;

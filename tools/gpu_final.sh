@@ -9,6 +9,8 @@ ROUND=${ROUND:-r05}
 O=gpurun_out/$TAG
 mkdir -p $O profiles/$ROUND
 step() { local name=$1 t=$2; shift 2; echo "== $name $(date +%T)"; timeout -k 10 $t "$@" > $O/$name.log 2>&1; local rc=$?; echo "== $name rc=$rc"; if [ $rc -ne 0 ]; then tail -30 $O/$name.log; exit $rc; fi; }
+PART=${PART:-all}  # 1: calibration, tests, smoke, PMC passes; 2: bench lines, profiles, probes
+if [ $PART != 2 ]; then
 step calib 300 env OUT=$O/calib bash tools/calib.sh
 mkdir -p profiles/$ROUND/calib && cp $O/calib/calib_summary.json $O/calib/known.json $O/calib/pass*_counter_collection.csv profiles/$ROUND/calib/
 step pytest 400 env WBC_MARGINS_OUT=$O/parity_margins.json python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
@@ -20,6 +22,8 @@ for cb in stance_cold_b4096:4096 rl_random_b8192:8192 modes16_b16384:16384 trot_
   cp gpurun_out/pmc_${TAG}_$c/pmc_summary.json $O/pmc_$c.json
   cp $O/pmc_$c.json profiles/$ROUND/pmc_$c.json  # read by bench.py below
 done
+fi
+if [ $PART = 1 ]; then echo part1 done; exit 0; fi
 step bench 300 python bench.py --steps 50 --warmup 5
 step bench_extra 300 python bench.py --steps 20 --warmup 3 --extra --breakdown --no-cpu-baseline
 step prof 300 rocprofv3 --kernel-trace --stats -d $O/prof -o prof --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline
