@@ -4566,6 +4566,17 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) {
         }
     }
     UST(a, qp, 30);  // kernel entry (diagnostic build)
+#ifdef WBC_ISTAMPS
+    // placement and the constant clock, for the wave-schedule probe (tools/wave_sched.py): slots
+    // 39 / 40 / 41 = s_memrealtime at entry, HW_ID, XCC_ID; 42 / 43 = s_memrealtime, s_memtime at the
+    // end; 44 = the workgroup's index
+    if (lane_id() == 0) {
+        a.dbg[(size_t)qp * WBC_DBG_LEN + 39] = (double)__builtin_amdgcn_s_memrealtime();
+        a.dbg[(size_t)qp * WBC_DBG_LEN + 40] = (double)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+        a.dbg[(size_t)qp * WBC_DBG_LEN + 41] = (double)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);
+        a.dbg[(size_t)qp * WBC_DBG_LEN + 44] = (double)blockIdx.x;
+    }
+#endif
     // the robot's inputs (HBM) are requested before the model staging waits for its own loads
     double vin[(91 + UPD_SUB - 1) / UPD_SUB];
     load_inputs<UPD_SUB>(a, row, lane, vin);
@@ -4594,6 +4605,12 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) {
     if (fm)
         drain_fallbacks<2 + STF>((const KernelArgs*)__builtin_amdgcn_kernarg_segment_ptr(), fm, qp,
                            reinterpret_cast<SolveLds*>(&L));
+#ifdef WBC_ISTAMPS
+    if (lane_id() == 0) {
+        a.dbg[(size_t)qp * WBC_DBG_LEN + 42] = (double)__builtin_amdgcn_s_memrealtime();
+        a.dbg[(size_t)qp * WBC_DBG_LEN + 43] = (double)__builtin_amdgcn_s_memtime();
+    }
+#endif
 }
 
 // The resident control cycle (wbc_cycle with WBC_RESIDENT, B <= 4: one wave): the step above,
