@@ -204,6 +204,16 @@ def step_kernel(e):
     return "wbc_modes_kernel" if e.modes_per_wave() > 1 else "wbc_update_solve_kernel"
 
 
+def kernel_instance(e, config):
+    """Which instance of the step kernel ran: the engine launches the stance-only instance
+    (wbc_kernel_stance.hip, its own schedule) for a stateless step whose masks are all 15."""
+    if e.modes_per_wave() > 1:
+        return "wbc_modes_kernel"
+    if config.startswith("stance"):
+        return "wbc_update_solve_kernel<0, true> (stance-only: wbc_kernel_stance.hip)"
+    return "wbc_update_solve_kernel<0, false> (every contact mask)"
+
+
 def roofline_of(flops, kernel_ms, traffic=None, traffic_src=None, kernel="wbc_update_solve_kernel"):
     tf = flops / (kernel_ms * 1e-3) / 1e12
     return {"bound": "fp64_valu", "achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -524,6 +534,7 @@ def main():
                      "frac": tf_dom / FP64_PEAK_TFLOPS, "traffic": traffic.get(dom),
                      "traffic_source": traffic_src, "kernel": dom, "kernel_ms": dom_ms,
                      "kernels_ms": kernels, "step_kernels_ms": step_ms,
+                     "instance": kernel_instance(e, args.config),
                      "note": f"the step's one kernel ({dom}; its kernel_ms is the step's, HIP events "
                              "around back-to-back launches); fp64 VALU roof (no MFMA on this path; gfx950 fp64 "
                              "vector peak); SURVEY 8(d) algorithmic flops: F_dyn + F_asm per state, F_fact + F_tau + "

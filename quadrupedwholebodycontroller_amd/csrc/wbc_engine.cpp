@@ -21,6 +21,7 @@ extern "C" hipError_t wbc_launch_update(const wbc::KernelArgs* a, hipStream_t st
 extern "C" hipError_t wbc_launch_solve_general(const wbc::KernelArgs* a, hipStream_t st);
 extern "C" hipError_t wbc_launch_solve_stance(const wbc::KernelArgs* a, hipStream_t st);
 extern "C" hipError_t wbc_launch_update_solve(const wbc::KernelArgs* a, hipStream_t st);
+extern "C" hipError_t wbc_launch_stance_step(const wbc::KernelArgs* a, hipStream_t st);
 extern "C" hipError_t wbc_launch_modes(const wbc::KernelArgs* a, hipStream_t st);
 extern "C" hipError_t wbc_launch_reset(double* hist, const uint8_t* mask, int batch, hipStream_t st);
 extern "C" hipError_t wbc_launch_qmap(const uint8_t* masks, int batch, int32_t* map, hipStream_t st);
@@ -323,6 +324,17 @@ hipError_t begin_step16(wbc_engine* h, wbc::KernelArgs& a, uint32_t flags) {
     return wbc_launch_qmap(h->in_contacts, h->batch, h->d_qmap, h->stream);
 }
 
+// The default step's QPs are all stance QPs of the stance form: stateless, the engine's own masks
+// (copied by the host, counted at copy time), every one 15, no map and no mode hypotheses.
+bool step_all_stance(const wbc_engine* h, const wbc::KernelArgs& a) {
+#ifdef WBC_NO_STANCE_TU  // (A/B builds only: the mixed-form kernel for every step)
+    return false;
+#else
+    const bool own = h->in_contacts == h->d_contacts || (h->m_contacts && h->in_contacts == h->m_contacts);
+    return own && h->qmap_host && h->n_stance_own == h->batch && !a.stateful && !a.modes && !a.qmap;
+#endif
+}
+
 hipError_t launch_solves(wbc_engine* h, wbc::KernelArgs& a) {
     a.elim = h->elim ? 1 : 0;
     a.parity = h->elim_parity;
@@ -619,9 +631,12 @@ int32_t wbc_step(wbc_engine* h, uint32_t flags) {
     } else if (flags & WBC_FUSED) {
         WBC_HIP(wbc_launch_step(&a, h->stream));  // one robot per wave, the general method
     } else {
-        // default: one kernel, every QP reduced to 12 variables and solved in the update wave
+        // default: one kernel, every QP reduced to 12 variables and solved in the update wave; a
+        // stateless step whose masks the host knows to be all 15 (no map then) runs the stance-only
+        // instance, scheduled for it alone (wbc_kernel_stance.hip)
         WBC_HIP(begin_step16(h, a, flags));
-        WBC_HIP(wbc_launch_update_solve(&a, h->stream));
+        if (step_all_stance(h, a)) WBC_HIP(wbc_launch_stance_step(&a, h->stream));
+        else WBC_HIP(wbc_launch_update_solve(&a, h->stream));
     }
     if (timed) {
         WBC_HIP(hipEventRecord(h->ev1, h->stream));

@@ -2318,7 +2318,7 @@ __device__ __forceinline__ void leg_bounds(double kr1, double ksw, double ko, do
     rsw = cmd - js_dot;
 }
 
-template <int SUB, bool SOLVE = false, typename Model = wbc_model, bool MLOOP = false, int STF = -1>
+template <int SUB, bool SOLVE = false, typename Model = wbc_model, bool MLOOP = false, int STF = -1, bool SONLY = false>
 __device__ __forceinline__ bool update_phase(const KernelArgs& a, int rb, int qp, int kap, int lane, bool wr, UpdScratch& s, Prob& P,
                              Presolve* pre, const Model& md, const double* fric = nullptr,
                              const double* vin = nullptr, int chunk = 0, unsigned* fails = nullptr) {
@@ -3129,7 +3129,9 @@ __device__ __forceinline__ bool update_phase(const KernelArgs& a, int rb, int qp
         // on stateful steps).  The choice is the segment's own, so a QP's result never depends on
         // its wave-mates; the wave map (KernelArgs::qmap) gives every wave one mask, so the branch
         // does not diverge (a mixed wave, from unmapped device-bound masks, runs both forms)
-        if (!stateful && kap == 15) {
+        // SONLY (wbc_stance_step_kernel: a stateless step whose masks are all 15, which the host
+        // knows): the stance form only, the general form compiled out
+        if (SONLY || (!stateful && kap == 15)) {
             double hrow[12], gsv = 0.0;
             if (stance_reduce<true>(a, rb, P, pr, lane, wr, s, hrow, gsv, nullptr) && rank6_factor(P, s, gsv, lane)) {
                 UST(a, rb, 11);
@@ -3138,6 +3140,7 @@ __device__ __forceinline__ bool update_phase(const KernelArgs& a, int rb, int qp
             }
             return false;
         }
+        if constexpr (SONLY) return false;
         const St16 V(s, P, fric);
         bool vac = false;
         if (reduce_general(a, rb, P, pr, lane, kap, s, V, vac)) {
@@ -4400,6 +4403,7 @@ struct SolveLds {
     QpScratch q;
 };
 
+#ifndef WBC_STANCE_TU  // (the stance TU, wbc_kernel_stance.hip, builds the stance-only step alone)
 WBC_KERNEL_ATTR void wbc_step_kernel(KernelArgs a) {
     __shared__ Lds L;
     const int rb = xcd_robot();
@@ -4410,6 +4414,7 @@ WBC_KERNEL_ATTR void wbc_step_kernel(KernelArgs a) {
     solve_phase(a, rb, L.prob, nullptr, L.q);
     STAMP(a, rb, 6);
 }
+#endif  // WBC_STANCE_TU
 
 // The update kernel, and (SOLVE) its form that also solves the four-contact stance QPs whose
 // elimination succeeded (wbc_update_solve_kernel: stateless all-stance steps; the problem of such
@@ -4455,6 +4460,7 @@ __device__ __forceinline__ void stage_to_lds(double2* dst, const double2* src, i
     }
 }
 
+#ifndef WBC_STANCE_TU
 // The split update (wbc_update, WBC_SPLIT, the update of wbc_step_modes' split form): Prob +
 // Presolve records to HBM for wbc_solve_kernel / wbc_solve_stance_kernel.
 WBC_UPDATE_KERNEL_ATTR void wbc_update_kernel(KernelArgs a) {
@@ -4486,6 +4492,7 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_kernel(KernelArgs a) {
         }
     }
 }
+#endif  // WBC_STANCE_TU
 
 // The default wbc_step (and wbc_step_modes): one kernel per step, four QPs per wave, 16 lanes
 // each.  Segment seg of workgroup w is QP qp = 4 w + seg: its inputs and history are row qp, or,
@@ -4526,7 +4533,7 @@ __device__ __forceinline__ int xcd_block(int b, int n) {
     return x * per + min(x, rem) + i;
 }
 // Two instances: STF = 0 for stateless steps (no history code at all), 1 for stateful ones
-template <int STF>
+template <int STF, bool SONLY = false>
 WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) {
     __shared__ UpdLds L;
     const int seg = (int)threadIdx.x / UPD_SUB, lane = (int)threadIdx.x % UPD_SUB;
@@ -4584,8 +4591,8 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_solve_kernel(KernelArgs a) {
     stage_to_lds<LIMG_LEN>(reinterpret_cast<double*>(&L), a.limg, (int)threadIdx.x);
     if (__all(empty)) return;  // the unused tail of a device-built map (uniform)
     lds_sync();
-    const bool solved = update_phase<UPD_SUB, true, LdsModel, false, STF>(a, row, qp, kap, lane, wr, L.u[seg], L.prob[seg], nullptr, L.model,
-                                                    &L.fric[0], vin);
+    const bool solved = update_phase<UPD_SUB, true, LdsModel, false, STF, SONLY>(a, row, qp, kap, lane, wr, L.u[seg], L.prob[seg], nullptr,
+                                                                         L.model, &L.fric[0], vin);
     // a QP whose reduction was not usable: its problem goes to work row qp, and the wave solves it
     // with the general 24-variable method right here (drain_fallbacks, the rare path; the wave's
     // LDS is reused once the four segments are done)
@@ -4724,6 +4731,7 @@ WBC_UPDATE_KERNEL_ATTR void wbc_resident_kernel(KernelArgs args, ResidentBox* bo
     }
 }
 
+#ifndef WBC_STANCE_TU
 // Mode hypotheses with the update shared (KernelArgs::mloop = M > 1): workgroup g C + c (C = K / M
 // chunks, xcd_block order, so a state group's chunks share an L2) runs states 4 g .. 4 g + 3, each
 // segment through one update and then the M hypotheses of chunk c (update_phase's mode loop);
@@ -4754,6 +4762,7 @@ WBC_UPDATE_KERNEL_ATTR void wbc_modes_kernel(KernelArgs a) {
     }
 }
 
+#endif  // WBC_STANCE_TU
 // Four-contact QP whose equalities the update kernel eliminated (its Presolve::stance flag, in
 // the record registers): wbc_solve_stance_kernel's; every other QP is wbc_solve_kernel's.
 __device__ __forceinline__ int qp_mask(const KernelArgs& a, int rb, int row) {
@@ -4762,6 +4771,7 @@ __device__ __forceinline__ int qp_mask(const KernelArgs& a, int rb, int row) {
 
 __device__ void solve_general_qp(const KernelArgs& a, int rb, SolveLds& L);
 
+#ifndef WBC_STANCE_TU
 WBC_KERNEL_ATTR void wbc_solve_kernel(KernelArgs a) {
     __shared__ SolveLds L;
     const int rb = xcd_robot();
@@ -4782,6 +4792,8 @@ WBC_KERNEL_ATTR void wbc_solve_fallback_kernel(KernelArgs a) {
         solve_general_qp(a, rb, L);
     }
 }
+
+#endif  // WBC_STANCE_TU
 
 __device__ void solve_general_qp(const KernelArgs& a, int rb, SolveLds& L) {
     // mode hypotheses: QP rb is hypothesis rb % modes of state rb / modes (one assembled problem
@@ -4812,6 +4824,7 @@ __device__ void solve_general_qp(const KernelArgs& a, int rb, SolveLds& L) {
     solve_phase(a, rb, L.prob, &pf, L.q);
 }
 
+#ifndef WBC_STANCE_TU
 // Four-contact stance QPs whose equalities the update kernel eliminated (Presolve::stance) are
 // solved here, in the 12-variable force space; wbc_solve_kernel skips them.  A kernel of its own
 // so that its register and LDS budgets (no 24-variable state, no LDS copy of the problem) allow
@@ -5012,8 +5025,19 @@ __global__ void wbc_reset_kernel(double* hist, const uint8_t* mask, int batch) {
     double* H = hist + (size_t)rb * HIST_LEN;
     for (int k = threadIdx.x; k < HIST_LEN; k += blockDim.x) H[k] = (k == H_KOLD) ? 15.0 : 0.0;
 }
+#endif  // WBC_STANCE_TU
 
 }  // namespace wbc
+
+#ifdef WBC_STANCE_TU
+// The stance-only default step (wbc_kernel_stance.hip): built in a translation unit of its own so
+// that its schedule can be chosen apart from the mixed-form kernel's (Makefile STANCE_KFLAGS)
+extern "C" hipError_t wbc_launch_stance_step(const wbc::KernelArgs* a, hipStream_t st) {
+    if (a->nwaves <= 0 || a->stateful || a->modes || a->qmap) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((wbc::wbc_update_solve_kernel<0, true>), dim3(a->nwaves), dim3(64), 0, st, *a);
+    return hipGetLastError();
+}
+#else
 
 // Launchers used by the engine (wbc_engine.cpp); grid = one 64-lane workgroup per robot.
 extern "C" hipError_t wbc_launch_step(const wbc::KernelArgs* a, hipStream_t st) {
@@ -5090,3 +5114,4 @@ extern "C" hipError_t wbc_launch_reset(double* hist, const uint8_t* mask, int ba
     hipLaunchKernelGGL(wbc::wbc_reset_kernel, dim3(batch), dim3(64), 0, st, hist, mask, batch);
     return hipGetLastError();
 }
+#endif  // WBC_STANCE_TU

@@ -44,3 +44,27 @@ def test_step_kernels_scratch_free():
     assert any("update_solve" in n for n in names) and any("drain_fallbacks" in n for n in names)
     assert any("modes_kernel" in n for n in names)
     assert sum("resident_kernel" in n for n in names) == 2
+
+
+def test_stance_step_kernel_scratch_free():
+    """The stance-only default step (wbc_kernel_stance.hip, its own translation unit under the
+    Makefile's STANCE_KFLAGS scheduler) compiles scratch-free too, and holds only that kernel and
+    its fallback call."""
+    mk = open(os.path.join(CSRC, "Makefile")).read()
+    waves = re.search(r"^WAVES \?= (\d+)", mk, re.M).group(1)
+    kflags = re.search(r"^KFLAGS := (.*)$", mk, re.M).group(1).split()
+    sflags = re.search(r"^STANCE_KFLAGS := (.*)$", mk, re.M).group(1).split()
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-I", os.path.join(ROOT, "include"),
+                        "-I", CSRC, f"-DWBC_WAVES_PER_SIMD={waves}", *kflags, *sflags, "-S", "--offload-device-only",
+                        os.path.join(CSRC, "wbc_kernel_stance.hip"), "-o", "-"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = r.stdout.split("\n")
+    starts = [(i, l.split(":")[0]) for i, l in enumerate(lines) if re.match(r"^_Z\w+:", l)]
+    ends = [i for i, l in enumerate(lines) if l.startswith(".Lfunc_end")]
+    names = [n for _, n in starts]
+    assert len(names) == 2 and any("wbc_update_solve_kernelILi0ELb1E" in n for n in names), names
+    for i, n in starts:
+        if "drain_fallbacks" in n:
+            continue
+        body = lines[i:min(x for x in ends if x > i)]
+        assert not [l for l in body if "scratch_" in l], n

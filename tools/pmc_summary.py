@@ -22,8 +22,13 @@ def kernel_source_hash():
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     h = hashlib.sha256()
-    for f in ("wbc_kernel.hip", "wbc_layout.h"):
-        h.update(open(os.path.join(root, "quadrupedwholebodycontroller_amd", "csrc", f), "rb").read())
+    csrc = os.path.join(root, "quadrupedwholebodycontroller_amd", "csrc")
+    for f in ("wbc_kernel.hip", "wbc_kernel_stance.hip", "wbc_layout.h"):
+        h.update(open(os.path.join(csrc, f), "rb").read())
+    # the kernels' own compile flags (the stance TU's scheduler among them)
+    for line in open(os.path.join(csrc, "Makefile")):
+        if line.startswith(("KFLAGS :=", "STANCE_KFLAGS :=")):
+            h.update(line.encode())
     return h.hexdigest()
 
 
