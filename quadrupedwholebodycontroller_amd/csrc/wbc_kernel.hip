@@ -2394,8 +2394,11 @@ __device__ __forceinline__ bool update_phase(const KernelArgs& a, int rb, int qp
     constexpr int NT = (18 + SUB - 1) / SUB;  // Tdot_inv columns per lane
     double hTd[18], hMa[NT][6], hR[3], hDo[3], hJo[12], hE = 0.0, hv = 0.0, hk = 15.0;
     double hWlo = 0.0, hWhi = 0.0, hWtag = 0.0;  // the previous working set (solve16's hotstart)
-    auto load_hist = [&]() {
-        const int l6 = lane < 6 ? lane : 5, l12 = lane < 12 ? lane : 11;
+    // in two parts: the stateful default step issues them at the starts of stages B and Ic (all
+    // ~55 at once, at stage A's start, stalled the wave on their issue: stage A took 6.6 k ticks
+    // against 4.3 k without them, profiles/r05/hist_split/)
+    auto load_hist_a = [&]() {
+        const int l6 = lane < 6 ? lane : 5;
         hv = H[H_VALID];
         hk = H[H_KOLD];
         hWlo = H[H_WSLO];
@@ -2403,6 +2406,9 @@ __device__ __forceinline__ bool update_phase(const KernelArgs& a, int rb, int qp
         hWtag = H[H_WSKAP];
 #pragma unroll
         for (int cc = 0; cc < 18; ++cc) hTd[cc] = H[H_TDINV + l6 * 18 + cc];
+    };
+    auto load_hist_b = [&]() {
+        const int l6 = lane < 6 ? lane : 5, l12 = lane < 12 ? lane : 11;
 #pragma unroll
         for (int i = 0; i < 3; ++i) hR[i] = H[H_ROLD + i];
 #pragma unroll
@@ -2417,7 +2423,10 @@ __device__ __forceinline__ bool update_phase(const KernelArgs& a, int rb, int qp
         for (int j = 0; j < 12; ++j) hJo[j] = H[H_JBJOLD + l12 * 12 + j];
         hE = H[H_EINT + l6];
     };
-    if constexpr (STF == 1) load_hist();
+    auto load_hist = [&]() {
+        load_hist_a();
+        load_hist_b();
+    };
     const double* pB = &s.in[0];
     const double* vB = &s.in[7];
     const double* wB = &s.in[10];
@@ -2523,6 +2532,7 @@ __device__ __forceinline__ bool update_phase(const KernelArgs& a, int rb, int qp
     lds_sync();
 
     UST(a, rb, 2);
+    if constexpr (STF == 1) load_hist_a();
     // stage B: one lane per body: com, world inertia, com velocity, m a_com, I alpha + w x I w
     double c[3] = {0, 0, 0}, cd[3] = {0, 0, 0};  // CoM and its velocity (cpp:260-261)
     {
@@ -2603,6 +2613,7 @@ __device__ __forceinline__ bool update_phase(const KernelArgs& a, int rb, int qp
     for (int i = 0; i < 3; ++i) { c[i] *= inv_m; cd[i] *= inv_m; }
     const double r[3] = {c[0] - pB[0], c[1] - pB[1], c[2] - pB[2]};
     UST(a, rb, 4);
+    if constexpr (STF == 1) load_hist_b();
     double Ic[9], Icinv[9];
     {   // centroidal inertia: parallel-axis contributions of the 13 bodies, summed across lanes
         double t[6] = {0, 0, 0, 0, 0, 0};
