@@ -2953,7 +2953,11 @@ __device__ __forceinline__ bool update_phase(const KernelArgs& a, int rb, int qp
                  (k == 2 ? md.total_mass * pr.gravity : 0.0) + mba;
         if (stateful && wr) H[H_EINT + k] = eint + e * fast_rcp(pr.loop_rate);
     }
-    stateful ? wsync() : lds_sync();
+    // the default step's stateful instance only needs the LDS (P.Jbj) here: every read of the old
+    // history finished at the first barrier above, and these stores do not overlap the ones just
+    // issued, so waiting for those to complete (a full barrier's vmcnt(0)) only put a write round
+    // trip on the chain
+    (stateful && STF != 1) ? wsync() : lds_sync();
     if (stateful && wr) {
         for (int k = lane; k < 144; k += SUB) H[H_JBJOLD + k] = P.Jbj[k];
         if (lane < 12) H[H_DOLD + lane] = P.d[lane];
