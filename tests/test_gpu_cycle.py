@@ -179,3 +179,22 @@ def test_resident_cycle_then_plain_steps():
             assert np.array_equal(got[k], want[k]), (t, k)
     e1.close()
     e2.close()
+
+
+@pytest.mark.parametrize("B", [2, 4, 5])
+def test_resident_cycle_stateless_and_above_limit(B):
+    """WBC_RESIDENT | WBC_STATELESS: cold solves through the resident wave (mixed masks, then all
+    stance, then mixed again: the masks change between cycles) equal separate calls bit for bit.
+    B = 5 is above the resident limit (B <= 4): the flag falls back to the launch path, same bits."""
+    e1, e2 = Engine(B), Engine(B)
+    for t in range(6):
+        inp = workloads.rl_random(B, seed=70 + t)
+        if t in (2, 3):
+            inp["contacts"] = np.full(B, 15, np.uint8)
+        want = separate_calls(e1, inp, STATELESS)
+        got = e2.cycle(inp["base_pose"], inp["nu"], inp["qj"], inp["ref"], inp["contacts"], inp["switching"],
+                       RESIDENT | STATELESS)
+        for k in KEYS:
+            assert np.array_equal(got[k], want[k]), (t, k)
+    e1.close()
+    e2.close()
