@@ -1,5 +1,7 @@
 // wbc_kernel.hip — batched whole-body-control step for gfx950 (MI355X), fp64.
 //
+// (wbc_kernel_stance.hip includes this file under WBC_STANCE_TU to build the stance-only default
+// step, wbc_update_solve_kernel<0, true>, alone under its own schedule: DESIGN.md 4.22.)
 // The default step (wbc_update_solve_kernel, the mode loop wbc_modes_kernel and the resident B <= 4
 // cycle wbc_resident_kernel) runs four robots per 64-lane wavefront, a 16-lane segment each, one
 // workgroup = one wave, one wave per SIMD (≈ 400 registers, 40 KB of LDS), and solves each robot's

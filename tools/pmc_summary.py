@@ -23,8 +23,15 @@ def kernel_source_hash():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     h = hashlib.sha256()
     csrc = os.path.join(root, "quadrupedwholebodycontroller_amd", "csrc")
+    # the code, not its comments: a comment edit leaves the counters valid
+    import re
+
     for f in ("wbc_kernel.hip", "wbc_kernel_stance.hip", "wbc_layout.h"):
-        h.update(open(os.path.join(csrc, f), "rb").read())
+        text = open(os.path.join(csrc, f)).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        text = re.sub(r"//[^\n]*", "", text)
+        text = "\n".join(l.rstrip() for l in text.split("\n") if l.strip())
+        h.update(text.encode())
     # the kernels' own compile flags (the stance TU's scheduler among them)
     for line in open(os.path.join(csrc, "Makefile")):
         if line.startswith(("KFLAGS :=", "STANCE_KFLAGS :=")):
