@@ -205,13 +205,14 @@ def step_kernel(e):
 
 
 def kernel_instance(e, config):
-    """Which instance of the step kernel ran: the engine launches the stance-only instance
-    (wbc_kernel_stance.hip, its own schedule) for a stateless step whose masks are all 15."""
+    """Which instance of the step kernel ran, and its translation unit (each under its own
+    schedule): the engine launches the stance-only instance for a stateless
+    step whose masks are all 15, the mixed-form instance for any other stateless step."""
     if e.modes_per_wave() > 1:
-        return "wbc_modes_kernel"
+        return "wbc_modes_kernel (wbc_kernel_modes.hip)"
     if config.startswith("stance"):
         return "wbc_update_solve_kernel<0, true> (stance-only: wbc_kernel_stance.hip)"
-    return "wbc_update_solve_kernel<0, false> (every contact mask)"
+    return "wbc_update_solve_kernel<0, false> (every contact mask: wbc_kernel_step0.hip)"
 
 
 def roofline_of(flops, kernel_ms, traffic=None, traffic_src=None, kernel="wbc_update_solve_kernel"):

@@ -1,7 +1,9 @@
 // wbc_kernel.hip — batched whole-body-control step for gfx950 (MI355X), fp64.
 //
-// (wbc_kernel_stance.hip includes this file under WBC_STANCE_TU to build the stance-only default
-// step, wbc_update_solve_kernel<0, true>, alone under its own schedule: DESIGN.md 4.22.)
+// (Three translation units include this file to build one kernel each under its own schedule:
+// wbc_kernel_stance.hip the stance-only default step, wbc_update_solve_kernel<0, true> (DESIGN.md
+// 4.22); wbc_kernel_step0.hip the stateless default step, wbc_update_solve_kernel<0>; and
+// wbc_kernel_modes.hip the mode loop, wbc_modes_kernel (4.24).  This file's own unit builds the rest.)
 // The default step (wbc_update_solve_kernel, the mode loop wbc_modes_kernel and the resident B <= 4
 // cycle wbc_resident_kernel) runs four robots per 64-lane wavefront, a 16-lane segment each, one
 // workgroup = one wave, one wave per SIMD (≈ 400 registers, 40 KB of LDS), and solves each robot's
@@ -4420,7 +4422,13 @@ struct SolveLds {
     QpScratch q;
 };
 
-#ifndef WBC_STANCE_TU  // (the stance TU, wbc_kernel_stance.hip, builds the stance-only step alone)
+// The one-kernel translation units (wbc_kernel_stance.hip, wbc_kernel_step0.hip,
+// wbc_kernel_modes.hip) include this file under their own macro, which keeps only their kernel and
+// its launcher; this file's own unit builds everything else
+#if defined(WBC_STANCE_TU) || defined(WBC_STEP0_TU) || defined(WBC_MODES_TU)
+#define WBC_SINGLE_TU 1
+#endif
+#ifndef WBC_SINGLE_TU
 WBC_KERNEL_ATTR void wbc_step_kernel(KernelArgs a) {
     __shared__ Lds L;
     const int rb = xcd_robot();
@@ -4431,7 +4439,7 @@ WBC_KERNEL_ATTR void wbc_step_kernel(KernelArgs a) {
     solve_phase(a, rb, L.prob, nullptr, L.q);
     STAMP(a, rb, 6);
 }
-#endif  // WBC_STANCE_TU
+#endif  // WBC_SINGLE_TU
 
 // The update kernel, and (SOLVE) its form that also solves the four-contact stance QPs whose
 // elimination succeeded (wbc_update_solve_kernel: stateless all-stance steps; the problem of such
@@ -4477,7 +4485,7 @@ __device__ __forceinline__ void stage_to_lds(double2* dst, const double2* src, i
     }
 }
 
-#ifndef WBC_STANCE_TU
+#ifndef WBC_SINGLE_TU
 // The split update (wbc_update, WBC_SPLIT, the update of wbc_step_modes' split form): Prob +
 // Presolve records to HBM for wbc_solve_kernel / wbc_solve_stance_kernel.
 WBC_UPDATE_KERNEL_ATTR void wbc_update_kernel(KernelArgs a) {
@@ -4509,7 +4517,7 @@ WBC_UPDATE_KERNEL_ATTR void wbc_update_kernel(KernelArgs a) {
         }
     }
 }
-#endif  // WBC_STANCE_TU
+#endif  // WBC_SINGLE_TU
 
 // The default wbc_step (and wbc_step_modes): one kernel per step, four QPs per wave, 16 lanes
 // each.  Segment seg of workgroup w is QP qp = 4 w + seg: its inputs and history are row qp, or,
@@ -4748,7 +4756,7 @@ WBC_UPDATE_KERNEL_ATTR void wbc_resident_kernel(KernelArgs args, ResidentBox* bo
     }
 }
 
-#ifndef WBC_STANCE_TU
+#ifdef WBC_MODES_TU  // (wbc_kernel_modes.hip)
 // Mode hypotheses with the update shared (KernelArgs::mloop = M > 1): workgroup g C + c (C = K / M
 // chunks, xcd_block order, so a state group's chunks share an L2) runs states 4 g .. 4 g + 3, each
 // segment through one update and then the M hypotheses of chunk c (update_phase's mode loop);
@@ -4779,7 +4787,7 @@ WBC_UPDATE_KERNEL_ATTR void wbc_modes_kernel(KernelArgs a) {
     }
 }
 
-#endif  // WBC_STANCE_TU
+#endif  // WBC_MODES_TU
 // Four-contact QP whose equalities the update kernel eliminated (its Presolve::stance flag, in
 // the record registers): wbc_solve_stance_kernel's; every other QP is wbc_solve_kernel's.
 __device__ __forceinline__ int qp_mask(const KernelArgs& a, int rb, int row) {
@@ -4788,7 +4796,7 @@ __device__ __forceinline__ int qp_mask(const KernelArgs& a, int rb, int row) {
 
 __device__ void solve_general_qp(const KernelArgs& a, int rb, SolveLds& L);
 
-#ifndef WBC_STANCE_TU
+#ifndef WBC_SINGLE_TU
 WBC_KERNEL_ATTR void wbc_solve_kernel(KernelArgs a) {
     __shared__ SolveLds L;
     const int rb = xcd_robot();
@@ -4810,7 +4818,7 @@ WBC_KERNEL_ATTR void wbc_solve_fallback_kernel(KernelArgs a) {
     }
 }
 
-#endif  // WBC_STANCE_TU
+#endif  // WBC_SINGLE_TU
 
 __device__ void solve_general_qp(const KernelArgs& a, int rb, SolveLds& L) {
     // mode hypotheses: QP rb is hypothesis rb % modes of state rb / modes (one assembled problem
@@ -4841,7 +4849,7 @@ __device__ void solve_general_qp(const KernelArgs& a, int rb, SolveLds& L) {
     solve_phase(a, rb, L.prob, &pf, L.q);
 }
 
-#ifndef WBC_STANCE_TU
+#ifndef WBC_SINGLE_TU
 // Four-contact stance QPs whose equalities the update kernel eliminated (Presolve::stance) are
 // solved here, in the 12-variable force space; wbc_solve_kernel skips them.  A kernel of its own
 // so that its register and LDS budgets (no 24-variable state, no LDS copy of the problem) allow
@@ -5042,7 +5050,7 @@ __global__ void wbc_reset_kernel(double* hist, const uint8_t* mask, int batch) {
     double* H = hist + (size_t)rb * HIST_LEN;
     for (int k = threadIdx.x; k < HIST_LEN; k += blockDim.x) H[k] = (k == H_KOLD) ? 15.0 : 0.0;
 }
-#endif  // WBC_STANCE_TU
+#endif  // WBC_SINGLE_TU
 
 }  // namespace wbc
 
@@ -5054,7 +5062,23 @@ extern "C" hipError_t wbc_launch_stance_step(const wbc::KernelArgs* a, hipStream
     hipLaunchKernelGGL((wbc::wbc_update_solve_kernel<0, true>), dim3(a->nwaves), dim3(64), 0, st, *a);
     return hipGetLastError();
 }
+#elif defined(WBC_STEP0_TU)
+// The stateless default step of any mask mix (wbc_kernel_step0.hip: both forms, its own schedule,
+// Makefile STEP0_KFLAGS; wbc_launch_update_solve below forwards its stateless steps here)
+extern "C" hipError_t wbc_launch_update_solve0(const wbc::KernelArgs* a, hipStream_t st) {
+    if (a->nwaves <= 0 || a->stateful) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(wbc::wbc_update_solve_kernel<0>, dim3(a->nwaves), dim3(64), 0, st, *a);
+    return hipGetLastError();
+}
+#elif defined(WBC_MODES_TU)
+// The mode loop (wbc_kernel_modes.hip, Makefile MODES_KFLAGS)
+extern "C" hipError_t wbc_launch_modes(const wbc::KernelArgs* a, hipStream_t st) {
+    if (a->nwaves <= 0 || a->modes <= 0 || a->mloop <= 0 || a->modes % a->mloop != 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(wbc::wbc_modes_kernel, dim3(a->nwaves), dim3(64), 0, st, *a);
+    return hipGetLastError();
+}
 #else
+extern "C" hipError_t wbc_launch_update_solve0(const wbc::KernelArgs* a, hipStream_t st);
 
 // Launchers used by the engine (wbc_engine.cpp); grid = one 64-lane workgroup per robot.
 extern "C" hipError_t wbc_launch_step(const wbc::KernelArgs* a, hipStream_t st) {
@@ -5090,18 +5114,11 @@ extern "C" hipError_t wbc_launch_solve_stance(const wbc::KernelArgs* a, hipStrea
 // The default step in one launch: the update kernel reducing and solving every QP inline, and the
 // QPs whose reduction was not usable with the general method in the same wave (drain_fallbacks:
 // their records carry their own mask and bounds, so the general solve runs them with modes = 0).
-extern "C" hipError_t wbc_launch_modes(const wbc::KernelArgs* a, hipStream_t st) {
-    if (a->nwaves <= 0 || a->modes <= 0 || a->mloop <= 0 || a->modes % a->mloop != 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(wbc::wbc_modes_kernel, dim3(a->nwaves), dim3(64), 0, st, *a);
-    return hipGetLastError();
-}
 extern "C" hipError_t wbc_launch_update_solve(const wbc::KernelArgs* a, hipStream_t st) {
     static_assert(wbc::UPD_RPW == wbc::QMAP_SEG, "the wave map's segments are the kernel's");
     if (a->nwaves <= 0) return hipErrorInvalidValue;
-    if (a->stateful)
-        hipLaunchKernelGGL(wbc::wbc_update_solve_kernel<1>, dim3(a->nwaves), dim3(64), 0, st, *a);
-    else
-        hipLaunchKernelGGL(wbc::wbc_update_solve_kernel<0>, dim3(a->nwaves), dim3(64), 0, st, *a);
+    if (!a->stateful) return wbc_launch_update_solve0(a, st);
+    hipLaunchKernelGGL(wbc::wbc_update_solve_kernel<1>, dim3(a->nwaves), dim3(64), 0, st, *a);
     return hipGetLastError();
 }
 // The resident control cycle (one workgroup, B <= 4), until WBC_RESIDENT_STOP or idle_ticks without a command
@@ -5131,4 +5148,4 @@ extern "C" hipError_t wbc_launch_reset(double* hist, const uint8_t* mask, int ba
     hipLaunchKernelGGL(wbc::wbc_reset_kernel, dim3(batch), dim3(64), 0, st, hist, mask, batch);
     return hipGetLastError();
 }
-#endif  // WBC_STANCE_TU
+#endif  // WBC_STANCE_TU / WBC_STEP0_TU / WBC_MODES_TU

@@ -7,6 +7,8 @@ import os
 import re
 import subprocess
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "quadrupedwholebodycontroller_amd", "csrc")
 
@@ -41,28 +43,38 @@ def test_step_kernels_scratch_free():
         calls = [l for l in body if "s_swappc" in l]
         assert not calls or "update_solve" in n or "modes_kernel" in n or "resident_kernel" in n, (n, calls)
     assert any("solve_stance" in n for n in names)
-    assert any("update_solve" in n for n in names) and any("drain_fallbacks" in n for n in names)
-    assert any("modes_kernel" in n for n in names)
+    assert any("update_solve_kernelILi1E" in n for n in names) and any("drain_fallbacks" in n for n in names)
+    # the stateless default step and the mode loop live in their own units (the test below)
+    assert not any("update_solve_kernelILi0E" in n or "modes_kernel" in n for n in names), names
     assert sum("resident_kernel" in n for n in names) == 2
 
 
-def test_stance_step_kernel_scratch_free():
-    """The stance-only default step (wbc_kernel_stance.hip, its own translation unit under the
-    Makefile's STANCE_KFLAGS scheduler) compiles scratch-free too, and holds only that kernel and
-    its fallback call."""
+UNITS = {  # one-kernel translation unit -> (its Makefile flags variable, the kernel's mangled name)
+    "stance": ("STANCE_KFLAGS", "wbc_update_solve_kernelILi0ELb1E"),
+    "step0": ("STEP0_KFLAGS", "wbc_update_solve_kernelILi0ELb0E"),
+    "modes": ("MODES_KFLAGS", "wbc_modes_kernel"),
+}
+
+
+@pytest.mark.parametrize("unit", sorted(UNITS))
+def test_one_kernel_units_scratch_free(unit):
+    """The one-kernel units (wbc_kernel_stance.hip, wbc_kernel_step0.hip, wbc_kernel_modes.hip, each
+    under its own Makefile flags) compile scratch-free too, and each holds
+    only its kernel and that kernel's fallback call."""
+    var, kname = UNITS[unit]
     mk = open(os.path.join(CSRC, "Makefile")).read()
     waves = re.search(r"^WAVES \?= (\d+)", mk, re.M).group(1)
     kflags = re.search(r"^KFLAGS := (.*)$", mk, re.M).group(1).split()
-    sflags = re.search(r"^STANCE_KFLAGS := (.*)$", mk, re.M).group(1).split()
+    sflags = re.search(rf"^{var} := (.*)$", mk, re.M).group(1).split()
     r = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-I", os.path.join(ROOT, "include"),
                         "-I", CSRC, f"-DWBC_WAVES_PER_SIMD={waves}", *kflags, *sflags, "-S", "--offload-device-only",
-                        os.path.join(CSRC, "wbc_kernel_stance.hip"), "-o", "-"], capture_output=True, text=True, timeout=600)
+                        os.path.join(CSRC, f"wbc_kernel_{unit}.hip"), "-o", "-"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = r.stdout.split("\n")
     starts = [(i, l.split(":")[0]) for i, l in enumerate(lines) if re.match(r"^_Z\w+:", l)]
     ends = [i for i, l in enumerate(lines) if l.startswith(".Lfunc_end")]
     names = [n for _, n in starts]
-    assert len(names) == 2 and any("wbc_update_solve_kernelILi0ELb1E" in n for n in names), names
+    assert len(names) == 2 and any(kname in n for n in names) and any("drain_fallbacks" in n for n in names), names
     for i, n in starts:
         if "drain_fallbacks" in n:
             continue

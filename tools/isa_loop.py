@@ -1,5 +1,6 @@
-"""Static instruction counts of the active-set loops of wbc_update_solve_kernel<0> (the headline
-step), per basic block, from the `make listing` output (hipcc -S -gline-tables-only).
+"""Static instruction counts of the active-set loops of wbc_update_solve_kernel<0> (the stateless
+default step, wbc_kernel_step0.hip), per basic block, from the `make listing` output (hipcc -S
+-gline-tables-only; the stance-only step: build/wbc_kernel_stance.s with --sym of its instance).
 
 A loop is the set of blocks the listing marks "in Loop: Header=BB..": the stance form's and the
 general form's loops.  For each, prints every block (instructions, VALU / DPP / LDS / SALU / waits /
@@ -11,7 +12,7 @@ import collections
 import re
 import sys
 
-SYM = "_ZN3wbc23wbc_update_solve_kernelILi0EEEvNS_10KernelArgsE"
+SYM = "_ZN3wbc23wbc_update_solve_kernelILi0ELb0EEEvNS_10KernelArgsE"
 
 
 def drop_lines(src):
@@ -25,7 +26,7 @@ def drop_lines(src):
 
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
-    path = args[0] if args else "quadrupedwholebodycontroller_amd/csrc/build/wbc_kernel.s"
+    path = args[0] if args else "quadrupedwholebodycontroller_amd/csrc/build/wbc_kernel_step0.s"
     sym = SYM
     if "--sym" in sys.argv:
         sym = sys.argv[sys.argv.index("--sym") + 1]

@@ -26,15 +26,15 @@ def kernel_source_hash():
     # the code, not its comments: a comment edit leaves the counters valid
     import re
 
-    for f in ("wbc_kernel.hip", "wbc_kernel_stance.hip", "wbc_layout.h"):
+    for f in ("wbc_kernel.hip", "wbc_kernel_stance.hip", "wbc_kernel_step0.hip", "wbc_kernel_modes.hip", "wbc_layout.h"):
         text = open(os.path.join(csrc, f)).read()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         text = re.sub(r"//[^\n]*", "", text)
         text = "\n".join(l.rstrip() for l in text.split("\n") if l.strip())
         h.update(text.encode())
-    # the kernels' own compile flags (the stance TU's scheduler among them)
+    # the kernels' own compile flags (the one-kernel units' schedulers among them)
     for line in open(os.path.join(csrc, "Makefile")):
-        if line.startswith(("KFLAGS :=", "STANCE_KFLAGS :=")):
+        if line.startswith(("KFLAGS :=", "STANCE_KFLAGS :=", "STEP0_KFLAGS :=", "MODES_KFLAGS :=")):
             h.update(line.encode())
     return h.hexdigest()
 
