@@ -4425,7 +4425,8 @@ struct SolveLds {
 // The one-kernel translation units (wbc_kernel_stance.hip, wbc_kernel_step0.hip,
 // wbc_kernel_modes.hip) include this file under their own macro, which keeps only their kernel and
 // its launcher; this file's own unit builds everything else
-#if defined(WBC_STANCE_TU) || defined(WBC_STEP0_TU) || defined(WBC_MODES_TU)
+#if defined(WBC_STANCE_TU) || defined(WBC_STEP0_TU) || defined(WBC_STEP1_TU) || defined(WBC_MODES_TU) || \
+    defined(WBC_RESIDENT_TU)
 #define WBC_SINGLE_TU 1
 #endif
 #ifndef WBC_SINGLE_TU
@@ -5077,8 +5078,42 @@ extern "C" hipError_t wbc_launch_modes(const wbc::KernelArgs* a, hipStream_t st)
     hipLaunchKernelGGL(wbc::wbc_modes_kernel, dim3(a->nwaves), dim3(64), 0, st, *a);
     return hipGetLastError();
 }
+#elif defined(WBC_STEP1_TU)
+// The stateful default step (wbc_kernel_step1.hip, Makefile STEP1_KFLAGS; wbc_launch_update_solve
+// below forwards its stateful steps here)
+extern "C" hipError_t wbc_launch_update_solve1(const wbc::KernelArgs* a, hipStream_t st) {
+    if (a->nwaves <= 0 || !a->stateful) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(wbc::wbc_update_solve_kernel<1>, dim3(a->nwaves), dim3(64), 0, st, *a);
+    return hipGetLastError();
+}
+#elif defined(WBC_RESIDENT_TU)
+// (wbc_kernel_resident.hip, Makefile RESIDENT_KFLAGS)
+// The resident control cycle (one workgroup, B <= 4), until WBC_RESIDENT_STOP or idle_ticks without a command
+extern "C" hipError_t wbc_launch_resident(const wbc::KernelArgs* a, wbc::ResidentBox* box, const void* pin_in,
+                                          void* own_in, int in_words, unsigned long long seq0, unsigned long long idle_ticks,
+                                          hipStream_t st) {
+    // B <= 4: the 2 B mask bytes fit the one word after the 91 B doubles
+    if (a->batch <= 0 || a->batch > wbc::UPD_RPW || a->qmap || a->modes || in_words != 91 * a->batch + 1)
+        return hipErrorInvalidValue;
+    const auto* pin = static_cast<const unsigned long long*>(pin_in);
+    auto* own = static_cast<unsigned long long*>(own_in);
+    if (a->stateful)
+        hipLaunchKernelGGL(wbc::wbc_resident_kernel<1>, dim3(1), dim3(64), 0, st, *a, box, pin, own, in_words, seq0, idle_ticks);
+    else
+        hipLaunchKernelGGL(wbc::wbc_resident_kernel<0>, dim3(1), dim3(64), 0, st, *a, box, pin, own, in_words, seq0, idle_ticks);
+    return hipGetLastError();
+}
+// Loads the resident kernels' code now (small engines: the B = 1 drop-in), so that the first resident
+// cycle does not pay the code object's lazy load (~10 ms, which showed in the control loop's mean)
+extern "C" hipError_t wbc_preload_resident() {
+    hipFuncAttributes at;
+    hipError_t e = hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&wbc::wbc_resident_kernel<1>));
+    if (e == hipSuccess) e = hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&wbc::wbc_resident_kernel<0>));
+    return e;
+}
 #else
 extern "C" hipError_t wbc_launch_update_solve0(const wbc::KernelArgs* a, hipStream_t st);
+extern "C" hipError_t wbc_launch_update_solve1(const wbc::KernelArgs* a, hipStream_t st);
 
 // Launchers used by the engine (wbc_engine.cpp); grid = one 64-lane workgroup per robot.
 extern "C" hipError_t wbc_launch_step(const wbc::KernelArgs* a, hipStream_t st) {
@@ -5117,35 +5152,10 @@ extern "C" hipError_t wbc_launch_solve_stance(const wbc::KernelArgs* a, hipStrea
 extern "C" hipError_t wbc_launch_update_solve(const wbc::KernelArgs* a, hipStream_t st) {
     static_assert(wbc::UPD_RPW == wbc::QMAP_SEG, "the wave map's segments are the kernel's");
     if (a->nwaves <= 0) return hipErrorInvalidValue;
-    if (!a->stateful) return wbc_launch_update_solve0(a, st);
-    hipLaunchKernelGGL(wbc::wbc_update_solve_kernel<1>, dim3(a->nwaves), dim3(64), 0, st, *a);
-    return hipGetLastError();
-}
-// The resident control cycle (one workgroup, B <= 4), until WBC_RESIDENT_STOP or idle_ticks without a command
-extern "C" hipError_t wbc_launch_resident(const wbc::KernelArgs* a, wbc::ResidentBox* box, const void* pin_in,
-                                          void* own_in, int in_words, unsigned long long seq0, unsigned long long idle_ticks,
-                                          hipStream_t st) {
-    // B <= 4: the 2 B mask bytes fit the one word after the 91 B doubles
-    if (a->batch <= 0 || a->batch > wbc::UPD_RPW || a->qmap || a->modes || in_words != 91 * a->batch + 1)
-        return hipErrorInvalidValue;
-    const auto* pin = static_cast<const unsigned long long*>(pin_in);
-    auto* own = static_cast<unsigned long long*>(own_in);
-    if (a->stateful)
-        hipLaunchKernelGGL(wbc::wbc_resident_kernel<1>, dim3(1), dim3(64), 0, st, *a, box, pin, own, in_words, seq0, idle_ticks);
-    else
-        hipLaunchKernelGGL(wbc::wbc_resident_kernel<0>, dim3(1), dim3(64), 0, st, *a, box, pin, own, in_words, seq0, idle_ticks);
-    return hipGetLastError();
-}
-// Loads the resident kernels' code now (small engines: the B = 1 drop-in), so that the first resident
-// cycle does not pay the code object's lazy load (~10 ms, which showed in the control loop's mean)
-extern "C" hipError_t wbc_preload_resident() {
-    hipFuncAttributes at;
-    hipError_t e = hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&wbc::wbc_resident_kernel<1>));
-    if (e == hipSuccess) e = hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&wbc::wbc_resident_kernel<0>));
-    return e;
+    return a->stateful ? wbc_launch_update_solve1(a, st) : wbc_launch_update_solve0(a, st);
 }
 extern "C" hipError_t wbc_launch_reset(double* hist, const uint8_t* mask, int batch, hipStream_t st) {
     hipLaunchKernelGGL(wbc::wbc_reset_kernel, dim3(batch), dim3(64), 0, st, hist, mask, batch);
     return hipGetLastError();
 }
-#endif  // WBC_STANCE_TU / WBC_STEP0_TU / WBC_MODES_TU
+#endif  // the one-kernel units

@@ -43,25 +43,27 @@ def test_step_kernels_scratch_free():
         calls = [l for l in body if "s_swappc" in l]
         assert not calls or "update_solve" in n or "modes_kernel" in n or "resident_kernel" in n, (n, calls)
     assert any("solve_stance" in n for n in names)
-    assert any("update_solve_kernelILi1E" in n for n in names) and any("drain_fallbacks" in n for n in names)
-    # the stateless default step and the mode loop live in their own units (the test below)
-    assert not any("update_solve_kernelILi0E" in n or "modes_kernel" in n for n in names), names
-    assert sum("resident_kernel" in n for n in names) == 2
+    # the default step's instances, the mode loop and the resident cycle live in their own units (the
+    # test below); this one holds the split and one-robot-per-wave forms, the map and reset kernels
+    assert not any(k in n for n in names for k in ("update_solve_kernel", "modes_kernel", "resident_kernel")), names
+    assert any("wbc_update_kernel" in n for n in names) and any("step_kernel" in n for n in names), names
 
 
-UNITS = {  # one-kernel translation unit -> (its Makefile flags variable, the kernel's mangled name)
-    "stance": ("STANCE_KFLAGS", "wbc_update_solve_kernelILi0ELb1E"),
-    "step0": ("STEP0_KFLAGS", "wbc_update_solve_kernelILi0ELb0E"),
-    "modes": ("MODES_KFLAGS", "wbc_modes_kernel"),
+UNITS = {  # one-kernel translation unit -> (its Makefile flags variable, its kernels' mangled names)
+    "stance": ("STANCE_KFLAGS", ["wbc_update_solve_kernelILi0ELb1E"]),
+    "step0": ("STEP0_KFLAGS", ["wbc_update_solve_kernelILi0ELb0E"]),
+    "step1": ("STEP1_KFLAGS", ["wbc_update_solve_kernelILi1ELb0E"]),
+    "modes": ("MODES_KFLAGS", ["wbc_modes_kernel"]),
+    "resident": ("RESIDENT_KFLAGS", ["wbc_resident_kernelILi0E", "wbc_resident_kernelILi1E"]),
 }
 
 
 @pytest.mark.parametrize("unit", sorted(UNITS))
 def test_one_kernel_units_scratch_free(unit):
-    """The one-kernel units (wbc_kernel_stance.hip, wbc_kernel_step0.hip, wbc_kernel_modes.hip, each
-    under its own Makefile flags) compile scratch-free too, and each holds
-    only its kernel and that kernel's fallback call."""
-    var, kname = UNITS[unit]
+    """The one-kernel units (wbc_kernel_<unit>.hip, each under its own Makefile flags, DESIGN.md
+    4.22 / 4.24) compile scratch-free too, and each holds only its kernel (the resident unit: the
+    two instances of its kernel) and the fallback call of each."""
+    var, knames = UNITS[unit]
     mk = open(os.path.join(CSRC, "Makefile")).read()
     waves = re.search(r"^WAVES \?= (\d+)", mk, re.M).group(1)
     kflags = re.search(r"^KFLAGS := (.*)$", mk, re.M).group(1).split()
@@ -74,7 +76,9 @@ def test_one_kernel_units_scratch_free(unit):
     starts = [(i, l.split(":")[0]) for i, l in enumerate(lines) if re.match(r"^_Z\w+:", l)]
     ends = [i for i, l in enumerate(lines) if l.startswith(".Lfunc_end")]
     names = [n for _, n in starts]
-    assert len(names) == 2 and any(kname in n for n in names) and any("drain_fallbacks" in n for n in names), names
+    kernels = [n for n in names if "drain_fallbacks" not in n]
+    assert len(kernels) == len(knames) and all(any(k in n for n in kernels) for k in knames), names
+    assert len(names) == 2 * len(knames), names  # one fallback callee per kernel
     for i, n in starts:
         if "drain_fallbacks" in n:
             continue

@@ -26,7 +26,8 @@ def kernel_source_hash():
     # the code, not its comments: a comment edit leaves the counters valid
     import re
 
-    for f in ("wbc_kernel.hip", "wbc_kernel_stance.hip", "wbc_kernel_step0.hip", "wbc_kernel_modes.hip", "wbc_layout.h"):
+    units = sorted(f for f in os.listdir(csrc) if f.startswith("wbc_kernel_") and f.endswith(".hip"))
+    for f in ["wbc_kernel.hip"] + units + ["wbc_layout.h"]:
         text = open(os.path.join(csrc, f)).read()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         text = re.sub(r"//[^\n]*", "", text)
@@ -34,7 +35,7 @@ def kernel_source_hash():
         h.update(text.encode())
     # the kernels' own compile flags (the one-kernel units' schedulers among them)
     for line in open(os.path.join(csrc, "Makefile")):
-        if line.startswith(("KFLAGS :=", "STANCE_KFLAGS :=", "STEP0_KFLAGS :=", "MODES_KFLAGS :=")):
+        if line.startswith("KFLAGS :=") or (line.split(" ", 1)[0].endswith("_KFLAGS") and ":=" in line):
             h.update(line.encode())
     return h.hexdigest()
 
