@@ -199,8 +199,8 @@ private:
     bool isSwitchingFootState_ = false;
 
     // one robot, per control cycle (profiles/r05/b1_*.log, mean / p99): the resident step
-    // (WBC_RESIDENT) 27.1 / 27.3 us, a launch per cycle (0) 34.4 / 38.8 us, WBC_FUSED (one robot
-    // per wave, the 24-variable form) 38.9 / 43.0 us
+    // (WBC_RESIDENT) 26.1 / 26.3 us, a launch per cycle (0) 34.0 / 37.8 us, WBC_FUSED (one robot
+    // per wave, the 24-variable form) 39.3 / 43.4 us
     uint32_t stepFlags_ = WBC_RESIDENT;
     int qpStatus_ = WBC_QP_OK;
     int qpIters_ = 0;
