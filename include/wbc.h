@@ -214,8 +214,14 @@ int32_t wbc_solve(wbc_engine* h, uint32_t flags);
  * Every form picks the row to add as the most violated one by slack / |reference row|, with near-
  * ties treated as ties: the lowest row id among the rows within WBC_TIE_BAND (relative) of the
  * most violated, so the route (and `iters`) does not depend on rounding when two rows are violated
- * alike in exact arithmetic.  The C oracle (oracle/wbc_ref.c) applies the same rule. */
+ * alike in exact arithmetic.  The C oracle (oracle/wbc_ref.c) applies the same rule.
+ * The general form (WBC_SPLIT / WBC_FUSED and the default step's fallback) also treats an r_k (the
+ * pending row's coefficient on active slot k) below WBC_R_REL times the largest |r| as zero, not as
+ * a drop candidate: when the pending row depends on the active set (an infeasible QP), those r_k
+ * are rounding noise, and the number of noise drops before WBC_QP_INFEASIBLE would otherwise
+ * depend on the form's rounding. */
 #define WBC_TIE_BAND 1e-9
+#define WBC_R_REL 1e-12
 int32_t wbc_step(wbc_engine* h, uint32_t flags);
 int32_t wbc_synchronize(wbc_engine* h);
 

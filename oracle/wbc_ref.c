@@ -291,9 +291,30 @@ void wbc_ref_kindyn(const wbc_model* md, const double* pose, const double* nu, c
  * inequality ids (for the next hotstart). */
 /* selnorm / tolv (may be NULL): the selection scale of each inequality (slack / selnorm; default
  * its row norm) and its violation tolerance (default 1e-10 max(1, |ci|)). */
+/* Diagnostic trace of the loop's decisions (tools/split_diverge.py): when set, each pass of the
+ * inequality loop appends TRACE_W doubles -- iteration, chosen row p, its scaled violation, the
+ * closest competing violation outside the tie band, t1, t2, the second-smallest drop ratio, n_p'z,
+ * the r[k] closest to the eps threshold, and the dropped row (-1 on an add) -- and the final pass
+ * the largest inactive slack / tolerance ratio.  Never set by the tests' checking paths. */
+#define TRACE_W 12
+static __thread double* g_trace;
+static __thread int g_trace_cap, g_trace_n;
+void wbc_ref_set_trace(double* buf, int cap) {
+    g_trace = buf;
+    g_trace_cap = cap;
+    g_trace_n = 0;
+}
+int wbc_ref_trace_len(void) { return g_trace_n; }
+static void trace_put(const double* v) {
+    if (g_trace && g_trace_n < g_trace_cap) {
+        memcpy(g_trace + (size_t)g_trace_n * TRACE_W, v, sizeof(double) * TRACE_W);
+        ++g_trace_n;
+    }
+}
+
 static int gi_solve(int n, const double* H, const double* g, int me, const double* CE, const double* ce, int mi,
                     const double* CI, const double* ci, int max_iter, const int* warm, int nwarm, double* x,
-                    int* iters_out, int* act_out, int* nact_out, const double* selnorm, const double* tolv) {
+                    int* iters_out, int* act_out, int* nact_out, const double* selnorm, const double* tolv, int rrel) {
     double L[NV * NV], J[NV * NV], R[NV * NV], u[NV], d[NV], z[NV], r[NV], ni[2 * NC], x0[NV];
     if (nact_out) *nact_out = 0;
     int act[NV]; /* >= 0: inequality id ; < 0: equality -(id+1) */
@@ -506,7 +527,25 @@ static int gi_solve(int n, const double* H, const double* g, int me, const doubl
             for (int i = 0; i < mi && p < 0; ++i)
                 if (wv[i] < 0.0 && wv[i] <= thr) p = i;
         }
-        if (p < 0) { *iters_out = iters; GI_RETURN(WBC_REF_OK); }
+        double tr[TRACE_W] = {0};
+        if (g_trace) {
+            /* closest competitor outside the band; closest inactive slack to its tolerance */
+            double second = 0.0, near = 0.0;
+            const double thr = best * (1.0 - WBC_TIE_BAND);
+            for (int i = 0; i < mi; ++i) {
+                if (wv[i] < 0.0 && wv[i] > thr && wv[i] < second) second = wv[i];
+                int isact = 0;
+                for (int k = n_eq; k < q; ++k)
+                    if (act[k] == i) { isact = 1; break; }
+                if (isact || wv[i] < 0.0) continue;
+                double sl = -ci[i];
+                for (int k = 0; k < n; ++k) sl += CI[i * n + k] * x[k];
+                const double tol = tolv ? tolv[i] : 1e-10 * (fabs(ci[i]) > 1.0 ? fabs(ci[i]) : 1.0);
+                if (-sl / tol > near) near = -sl / tol;
+            }
+            tr[0] = iters; tr[1] = p; tr[2] = best; tr[3] = second; tr[10] = near;
+        }
+        if (p < 0) { if (g_trace) { tr[1] = -2; trace_put(tr); } *iters_out = iters; GI_RETURN(WBC_REF_OK); }
         const double* np_ = CI + p * n;
         double sp = -ci[p];
         for (int k = 0; k < n; ++k) sp += np_[k] * x[k];
@@ -516,12 +555,36 @@ static int gi_solve(int n, const double* H, const double* g, int me, const doubl
             COMPUTE_DZR(np_);
             double t1 = INFINITY;
             int l = -1;
+            /* rrel (the literal / 24-variable form, WBC_R_REL): an r[k] that is rounding noise next to
+             * the largest |r| (a pending row dependent on the active set, z = 0: the infeasibility
+             * test) is not a drop candidate, so the two forms' different rounding cannot take
+             * different numbers of noise drops before INFEASIBLE */
+            double rthr = eps;
+            if (rrel) {
+                double rmax = 0.0;
+                for (int k = 0; k < q; ++k) rmax = fabs(r[k]) > rmax ? fabs(r[k]) : rmax;
+                if (WBC_R_REL * rmax > rthr) rthr = WBC_R_REL * rmax;
+            }
             for (int k = n_eq; k < q; ++k)
-                if (r[k] > eps && u[k] / r[k] < t1) { t1 = u[k] / r[k]; l = k; }
+                if (r[k] > rthr && u[k] / r[k] < t1) { t1 = u[k] / r[k]; l = k; }
             double zz = 0.0, zn = 0.0;
             for (int k = 0; k < n; ++k) zz += z[k] * z[k], zn += z[k] * np_[k];
             double t2 = (zz > eps * eps && zn > eps) ? -sp / zn : INFINITY;
             double t = t1 < t2 ? t1 : t2;
+            if (g_trace) {
+                double t1b = INFINITY, rnear = INFINITY, rmax = 0.0;
+                for (int k = 0; k < q; ++k) rmax = fabs(r[k]) > rmax ? fabs(r[k]) : rmax;
+                tr[11] = rmax;
+                for (int k = n_eq; k < q; ++k) {
+                    if (r[k] > eps && k != l && u[k] / r[k] < t1b) t1b = u[k] / r[k];
+                    const double ar = fabs(r[k]);
+                    if (ar > 1e-17 && fabs(log10(ar / eps)) < fabs(log10(rnear / eps))) rnear = ar;
+                }
+                tr[0] = iters; tr[4] = t1; tr[5] = t2; tr[6] = t1b; tr[7] = zn; tr[8] = rnear;
+                tr[9] = (isfinite(t2) && t == t2) ? -1 : (l >= 0 ? act[l] : -3);
+                trace_put(tr);
+                tr[1] = -1; tr[2] = tr[3] = 0.0;  /* a drop's next pass: same p, no new selection */
+            }
             if (!isfinite(t)) { *iters_out = iters; return WBC_REF_INFEASIBLE; }
             if (isfinite(t2)) {
                 for (int k = 0; k < n; ++k) x[k] += t * z[k];
@@ -602,13 +665,13 @@ static int solve_qp(const double* H, const double* g, const double* A, const dou
             ci[mi++] = -ub[i];
         }
     }
-    return gi_solve(n, H, g, me, CE, ce, mi, CI, ci, max_iter, warm, nwarm, x, iters, act_out, nact_out, NULL, NULL);
+    return gi_solve(n, H, g, me, CE, ce, mi, CI, ci, max_iter, warm, nwarm, x, iters, act_out, nact_out, NULL, NULL, 1);
 }
 
 /* The dense Goldfarb-Idnani above for other callers (oracle/wbc_fast.c), cold (no warm set). */
 int wbc_ref_gi(int n, const double* H, const double* g, int me, const double* CE, const double* ce, int mi, const double* CI,
                const double* ci, int max_iter, double* x, int* iters) {
-    return gi_solve(n, H, g, me, CE, ce, mi, CI, ci, max_iter, NULL, 0, x, iters, NULL, NULL, NULL, NULL);
+    return gi_solve(n, H, g, me, CE, ce, mi, CI, ci, max_iter, NULL, 0, x, iters, NULL, NULL, NULL, NULL, 0);
 }
 
 /* ------------------------------------------------------------------ the engine's 12-variable form */
@@ -840,7 +903,7 @@ static int reduced_solve(const wbc_params* pr, wbc_ref_state* st, const wbc_ref_
     double z[NV]; /* gi_solve saves and restores NV entries (warm start) */
     int act[NV], nact = 0;
     const int status = gi_solve(12, H, g, 0, NULL, NULL, mi, CI, ci, pr->max_wsr, nwarm ? warm : NULL, nwarm, z, iters, act,
-                                &nact, seln, tolv);
+                                &nact, seln, tolv, 0);
     st->ws12 = 0;
     st->ws12_valid = 1;
     if (status == WBC_REF_OK)
@@ -1148,5 +1211,22 @@ void wbc_ref_run_batch_method(const wbc_model* md, const wbc_params* pr, int B, 
         status[b] = wbc_ref_step(md, pr, &st, pose + 7 * b, nu + 18 * b, qj + 12 * b, ref + 54 * b, contacts[b],
                                  switching[b], tau + 12 * b, grf + 12 * b, x + NV * b, &it, NULL);
         iters[b] = it;
+    }
+}
+
+/* n stateful robots stepped together (the per-robot `Robot` of oracle/wbc_ref.py, one call per
+ * cycle): robot i reads row idx[i] of the batch input arrays and writes row i of the outputs.
+ * The tests use it to follow a sample of a large batch through a whole trajectory. */
+void wbc_ref_step_states(const wbc_model* md, const wbc_params* pr, int n, wbc_ref_state* st, const int32_t* idx,
+                         const double* pose, const double* nu, const double* qj, const double* ref,
+                         const uint8_t* contacts, const uint8_t* switching, double* tau, double* grf, double* x,
+                         int32_t* status, int32_t* iters, int threads) {
+#pragma omp parallel for schedule(dynamic, 4) num_threads(threads > 0 ? threads : 1)
+    for (int i = 0; i < n; ++i) {
+        const int b = idx[i];
+        int it = 0;
+        status[i] = wbc_ref_step(md, pr, st + i, pose + 7 * b, nu + 18 * b, qj + 12 * b, ref + 54 * b, contacts[b],
+                                 switching[b], tau + 12 * i, grf + 12 * i, x + NV * i, &it, NULL);
+        iters[i] = it;
     }
 }

@@ -44,6 +44,11 @@ void wbc_ref_run_batch(const wbc_model* md, const wbc_params* pr, int B, const d
 void wbc_ref_run_batch_method(const wbc_model* md, const wbc_params* pr, int B, const double* pose, const double* nu,
                               const double* qj, const double* ref, const uint8_t* contacts, const uint8_t* switching,
                               double* tau, double* grf, double* x, int32_t* status, int32_t* iters, int method);
+/* n stateful robots in one call: robot i (state st[i]) reads batch row idx[i], writes output row i */
+void wbc_ref_step_states(const wbc_model* md, const wbc_params* pr, int n, wbc_ref_state* st, const int32_t* idx,
+                         const double* pose, const double* nu, const double* qj, const double* ref,
+                         const uint8_t* contacts, const uint8_t* switching, double* tau, double* grf, double* x,
+                         int32_t* status, int32_t* iters, int threads);
 int wbc_ref_gi(int n, const double* H, const double* g, int me, const double* CE, const double* ce, int mi, const double* CI,
                const double* ci, int max_iter, double* x, int* iters);
 

@@ -56,6 +56,7 @@ def lib():
         _lib.wbc_ref_step.restype = C.c_int
         _lib.wbc_ref_run_batch.argtypes = [P, P, C.c_int, P, P, P, P, P, P, P, P, P, P, P]
         _lib.wbc_ref_run_batch_method.argtypes = [P, P, C.c_int, P, P, P, P, P, P, P, P, P, P, P, C.c_int]
+        _lib.wbc_ref_step_states.argtypes = [P, P, C.c_int, P, P, P, P, P, P, P, P, P, P, P, P, P, C.c_int]
         _bind_baseline(_lib)
     return _lib
 
@@ -216,4 +217,47 @@ class Robot:
         out = dict(tau=tau, grf=grf, x=x, status=st, iters=it.value)
         if debug:
             out["dbg"] = {k: np.array(getattr(dbg, k)) for k, _ in Debug._fields_}
+        return out
+
+
+class Robots:
+    """n stateful robots (each a `Robot`) stepped in one C call: robot i follows row idx[i] of the
+    batch inputs passed to step() (a sample of a large batch followed through a trajectory)."""
+
+    def __init__(self, idx, hotstart=True, method=LITERAL, threads=8, **overrides):
+        self.idx = np.ascontiguousarray(idx, np.int32)
+        n = len(self.idx)
+        self.st = (State * n)()
+        for i in range(n):
+            lib().wbc_ref_state_init(C.byref(self.st[i]))
+            self.st[i].cold_qp = 0 if hotstart else 1
+            self.st[i].method = int(method)
+        self.threads = threads
+        m, p = model_params()
+        if overrides:
+            p2 = type(p)()
+            C.pointer(p2)[0] = p
+            for k, v in overrides.items():
+                setattr(p2, k, v)
+            p = p2
+        self.m, self.p = m, p
+
+    def reset(self, which):
+        """setInitialState() for the robots i in `which` (sample positions)."""
+        for i in which:
+            cold, method = self.st[i].cold_qp, self.st[i].method
+            lib().wbc_ref_state_init(C.byref(self.st[i]))
+            self.st[i].cold_qp, self.st[i].method = cold, method
+
+    def step(self, inp):
+        n = len(self.idx)
+        f = lambda k, dt=np.float64: np.ascontiguousarray(inp[k], dt)
+        pose, nu, qj, ref = f("base_pose"), f("nu"), f("qj"), f("ref")
+        con, sw = f("contacts", np.uint8), f("switching", np.uint8)
+        assert int(self.idx.max()) < len(con)
+        out = dict(tau=np.zeros((n, 12)), grf=np.zeros((n, 12)), x=np.zeros((n, 42)), status=np.zeros(n, np.int32),
+                   iters=np.zeros(n, np.int32))
+        lib().wbc_ref_step_states(C.byref(self.m), C.byref(self.p), n, self.st, _p(self.idx), _p(pose), _p(nu), _p(qj),
+                                  _p(ref), _p(con), _p(sw), _p(out["tau"]), _p(out["grf"]), _p(out["x"]),
+                                  _p(out["status"]), _p(out["iters"]), int(self.threads))
         return out

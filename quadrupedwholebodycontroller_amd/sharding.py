@@ -62,15 +62,20 @@ class StepOutputs:
         self.iters[:n].copy_(torch.as_tensor(iters, dtype=torch.int32))
 
 
-def gather_step_outputs(block: StepOutputs, world: int, out=None, group=None):
+def gather_step_outputs(block: StepOutputs, world: int, out=None, group=None, collective=None):
     """The step's one collective: every rank's packed block, concatenated in rank order
     (RCCL all_gather_into_tensor on GPU tensors; the list form on gloo / CPU).  `out` is an
-    optional preallocated [world * 13 cap] fp64 tensor."""
+    optional preallocated [world * 13 cap] fp64 tensor.  With one rank there is nothing to gather
+    and the block is returned (copied into `out`) unless `collective` is True: then the collective
+    runs anyway (a one-rank process group), which is how tests/test_gpu_rccl.py executes the RCCL
+    branch on a one-GPU box."""
     import torch
     import torch.distributed as dist
 
     local = block.buf
-    if world == 1:
+    if collective is None:
+        collective = world > 1
+    if not collective:
         if out is not None:
             out.copy_(local)
             return out
@@ -140,16 +145,19 @@ class StepPipeline:
     whole batch's output).  tests/test_gpu_pipeline.py runs this class with two gloo ranks on one GPU
     and checks every step's gathered outputs against a one-rank step."""
 
-    def __init__(self, engine, step, flags, world, cap, stream, comm=None, device="cuda", group=None):
+    def __init__(self, engine, step, flags, world, cap, stream, comm=None, device="cuda", group=None, collective=None):
+        """collective: gather every step (default: world > 1); True with world == 1 runs the gather
+        path on a one-rank process group (tests/test_gpu_rccl.py)."""
         import torch
 
         self.torch = torch
         self.e, self.step_fn, self.flags, self.world = engine, step, flags, world
+        self.coll = (world > 1) if collective is None else bool(collective)
         self.stream, self.comm, self.group = stream, comm, group
         self.cap = cap
         self.blocks = [StepOutputs(cap, device=device) for _ in range(2)]
         self.gathered = ([torch.empty(world * cap * ROW_DOUBLES, dtype=torch.float64, device=device)
-                          for _ in range(2)] if world > 1 else None)
+                          for _ in range(2)] if self.coll else None)
         self.ev_step = [torch.cuda.Event() for _ in range(2)]
         self.ev_gath = [torch.cuda.Event() for _ in range(2)]
         self.used = [False, False]
@@ -163,15 +171,16 @@ class StepPipeline:
         """Queue one step (and, N > 1, its gather); returns the slot its outputs land in."""
         torch = self.torch
         slot = self.k & 1
-        if self.world > 1 and self.used[slot]:
+        if self.coll and self.used[slot]:
             self.stream.wait_event(self.ev_gath[slot])  # the gather of step k - 2 has read this block
         self.bind(slot)
         self.step_fn(self.flags)
-        if self.world > 1:
+        if self.coll:
             self.ev_step[slot].record(self.stream)
             with torch.cuda.stream(self.comm):
                 self.comm.wait_event(self.ev_step[slot])
-                gather_step_outputs(self.blocks[slot], self.world, out=self.gathered[slot], group=self.group)
+                gather_step_outputs(self.blocks[slot], self.world, out=self.gathered[slot], group=self.group,
+                                    collective=True)
                 self.ev_gath[slot].record(self.comm)
             self.used[slot] = True
         self.k += 1
@@ -186,7 +195,7 @@ class StepPipeline:
         gather is done; `total` QPs overall (N > 1) or this rank's (N = 1)."""
         import numpy as np
 
-        if self.world > 1:
+        if self.coll:
             self.ev_gath[slot].synchronize()
             return unpack_gathered(self.gathered[slot], total, self.world, unit=unit)
         self.ev_step[slot].record(self.stream)

@@ -1,4 +1,5 @@
-"""GPU parity at the bench's own sizes (BASELINE configs[1], the configs[3] and configs[4] shards).
+"""GPU parity at the bench's own sizes (BASELINE configs[1], configs[2] as bench.py times it, the
+configs[3] shard and its global batch on one GPU, the configs[4] shard).
 
 At B = 4096 and more the solve kernel runs several occupancy passes (8 robots per CU x 256 CUs
 per pass); the smaller parity tests fit in one.  Each test runs the full batch once, then:
@@ -61,7 +62,7 @@ def check_vs_oracle(out, rows, inp_rows):
         assert M.close(out["tau"][b], o["tau"][j], M.TAU, "tau"), (b, "tau")
 
 
-@pytest.mark.parametrize("name,B,seed", [("stance_cold", 4096, 1), ("rl_random", 8192, 3)])
+@pytest.mark.parametrize("name,B,seed", [("stance_cold", 4096, 1), ("rl_random", 8192, 3), ("rl_random", 65536, 3)])
 def test_full_batch_sample_matches_oracle_and_small_batch(name, B, seed):
     inp = getattr(workloads, name)(B, seed=seed)
     out = run(inp)
@@ -90,3 +91,61 @@ def test_modes_full_shard_sample_matches_oracle_and_small_batch():
     small = run({k: np.ascontiguousarray(v[states]) for k, v in inp.items()}, modes)
     for k in KEYS:
         assert np.array_equal(small[k], out[k][rows]), k
+
+
+def trot_rows(B, n=256):
+    """n robots spread over the batch, both sides of every 1024-robot boundary, every robot of the
+    first and last waves, and the last robot."""
+    rows = set(np.linspace(0, B - 1, n).astype(int).tolist())
+    for k in range(0, B + 1, 1024):
+        rows.update(r for r in (k - 2, k - 1, k, k + 1) if 0 <= r < B)
+    rows.update(range(4))
+    rows.update(range(B - 4, B))
+    return np.array(sorted(rows))
+
+
+def test_trot_bench_path_every_step_matches_stateful_oracle():
+    """BASELINE configs[2] exactly as bench.py times it (bench_trot): B = 4096 robots, 400 stateful
+    steps, all inputs staged in HBM and bound per step (wbc_bind_device_inputs), WBC_NO_X, the
+    history and hotstart carried on the GPU.  At every step >= 256 sampled robots are compared
+    with the C oracle's stateful robots (oracle/wbc_ref.c, the REDUCED method: the 12-variable form
+    with the same hotstart): identical status and iteration counts, tau / grf at the parity
+    tolerances.  The sequence then runs again after wbc_reset(), as bench.py's timed pass does after
+    its warm-up pass, and must reproduce the first pass bit for bit."""
+    import torch
+
+    from quadrupedwholebodycontroller_amd import NO_X
+
+    B, T = 4096, 400
+    seq = list(workloads.trot_sequence(B, steps=T, seed=2))  # bench_trot's inputs
+    dev = {k: torch.from_numpy(np.ascontiguousarray(np.stack([s[k] for s in seq]))).cuda() for k in seq[0]}
+    rows = trot_rows(B)
+    assert len(rows) >= 256 and rows[-1] == B - 1
+    e = Engine(B)
+    first = []
+    for p in range(2):
+        e.reset()
+        oracle = R.Robots(rows, method=R.REDUCED) if p == 0 else None
+        n_ok = n_it = 0
+        for t in range(T):
+            e.bind_device_inputs(dev["base_pose"][t].data_ptr(), dev["nu"][t].data_ptr(), dev["qj"][t].data_ptr(),
+                                 dev["ref"][t].data_ptr(), dev["contacts"][t].data_ptr(), dev["switching"][t].data_ptr())
+            e.step(NO_X)
+            g = e.outputs()
+            if p == 1:
+                for k in ("tau", "grf", "status", "iters"):
+                    assert np.array_equal(g[k], first[t][k]), (t, k)
+                continue
+            first.append({k: g[k].copy() for k in ("tau", "grf", "status", "iters")})
+            o = oracle.step(seq[t])
+            assert np.array_equal(g["status"][rows], o["status"]), (t, rows[g["status"][rows] != o["status"]][:8])
+            same = g["iters"][rows] == o["iters"]
+            assert M.record("iters mismatch fraction", 1.0 - same.mean(), 0.0) == 0.0, (t, rows[~same][:8])
+            ok = o["status"] == 0
+            assert M.close(g["tau"][rows][ok], o["tau"][ok], M.TAU, "tau"), t
+            assert M.close(g["grf"][rows][ok], o["grf"][ok], M.GRF, "grf"), t
+            n_ok += int(ok.sum())
+            n_it += int(o["iters"].sum())
+        if p == 0:
+            assert n_ok > 0.9 * len(rows) * T
+    e.close()
