@@ -140,6 +140,8 @@ public:
     // subscriber callbacks; a host's message source calls the *Callback methods from there or from
     // any other thread).  `loopHook(iteration)` runs on the control thread before every cycle.
     // Returns the cycles run.  Errors on the control thread (an engine failure) are rethrown here.
+    // Like controlLoop, run() does not clear the shutdown flag on entry (a requestShutdown() from
+    // another thread before run() ends it before its first cycle); resetShutdown() clears it.
     long run();
     void requestShutdown() { shutdown_.store(true); }
     void resetShutdown() { shutdown_.store(false); }

@@ -91,28 +91,57 @@ int run_stance(long cycles, double rate, uint32_t flags) {
     const JointState js = make_joint_state(q0, nu + 6);
     const WbcReferenceMsg rm = make_reference(ref, 15);
     wbc.floatingBaseStateCallback(ms);  // first message: locates the model only (cpp:189-204)
-    std::vector<double> lat;
+    std::vector<double> lat, work;
     lat.reserve(cycles);
+    work.reserve(cycles);
     auto t_prev = std::chrono::steady_clock::now();
     long n = 0;
-    n = wbc.controlLoop(cycles, rate, [&](long it) {
+    auto feed = [&](long it) {
         const auto now = std::chrono::steady_clock::now();
         if (it > 0) lat.push_back(std::chrono::duration<double, std::micro>(now - t_prev).count());
         t_prev = now;
         wbc.floatingBaseStateCallback(ms);
         wbc.jointStateCallback(js);
         wbc.referenceCallback(rm);
-    });
-    std::vector<double> s = lat;
-    std::sort(s.begin(), s.end());
-    auto pct = [&](double q) { return s.empty() ? 0.0 : s[std::min(s.size() - 1, (size_t)(q * s.size()))]; };
-    double mean = 0;
-    for (double v : lat) mean += v;
-    mean = lat.empty() ? 0 : mean / lat.size();
+    };
+    if (rate > 0.0) {
+        // a paced loop (ros::Rate): the same cycles as controlLoop, with each cycle's own time
+        // (controlCycle alone, without the sleep) recorded as work_us; at rates below the resident
+        // wave's restart limit (25 Hz) every cycle starts a new wave
+        wbc.setInitialState();
+        const auto period = std::chrono::duration_cast<std::chrono::steady_clock::duration>(
+            std::chrono::duration<double>(1.0 / rate));
+        auto next = std::chrono::steady_clock::now();
+        for (; n < cycles; ++n) {
+            feed(n);
+            const auto t0 = std::chrono::steady_clock::now();
+            wbc.controlCycle();
+            work.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+            if (wbc.qpReturnValue() != WBC_QP_OK) { ++n; break; }
+            next += period;
+            std::this_thread::sleep_until(next);
+        }
+    } else {
+        n = wbc.controlLoop(cycles, rate, feed);
+    }
+    auto stats = [](std::vector<double> s, double& mean, double& p50, double& p99) {
+        std::sort(s.begin(), s.end());
+        auto pct = [&](double q) { return s.empty() ? 0.0 : s[std::min(s.size() - 1, (size_t)(q * s.size()))]; };
+        mean = 0;
+        for (double v : s) mean += v;
+        mean = s.empty() ? 0 : mean / s.size();
+        p50 = pct(0.5);
+        p99 = pct(0.99);
+    };
+    double mean, p50, p99, wmean, w50, w99;
+    stats(lat, mean, p50, p99);
+    stats(work, wmean, w50, w99);
     const auto& tau = wbc.jointTorques();
     std::printf("{\"config\": \"stance_hold_b1\", \"cycles\": %ld, \"qp_status\": %d, \"qp_iters\": %d, "
-                "\"cycle_us_mean\": %.3f, \"cycle_us_p50\": %.3f, \"cycle_us_p99\": %.3f, \"rate_hz\": %.1f, \"tau\": [",
-                n, wbc.qpReturnValue(), wbc.qpIterations(), mean, pct(0.5), pct(0.99), rate);
+                "\"cycle_us_mean\": %.3f, \"cycle_us_p50\": %.3f, \"cycle_us_p99\": %.3f, \"rate_hz\": %.1f, ",
+                n, wbc.qpReturnValue(), wbc.qpIterations(), mean, p50, p99, rate);
+    if (rate > 0.0) std::printf("\"work_us_mean\": %.3f, \"work_us_p50\": %.3f, \"work_us_p99\": %.3f, ", wmean, w50, w99);
+    std::printf("\"tau\": [");
     for (int i = 0; i < numberOfJoints; ++i) std::printf("%s%.9g", i ? ", " : "", tau[i]);
     std::printf("]}\n");
     return wbc.qpReturnValue() == WBC_QP_OK ? 0 : 3;
@@ -156,9 +185,14 @@ int run_node(long cycles) {
     const long halted = wbc.controlLoop(25, 0.0, feed);
     wbc.resetShutdown();
     const long again = wbc.controlLoop(25, 0.0, feed);
+    // a shutdown requested before run() is not dropped by run() either: it runs no cycle
+    wbc.requestShutdown();
+    wbc.loopHook = nullptr;
+    const long pre = wbc.run();
+    wbc.resetShutdown();
     std::printf("{\"config\": \"node_run\", \"cycles\": %ld, \"control_loop_after_shutdown\": %ld, "
-                "\"control_loop_after_run\": %ld, \"qp_status\": %d, "
-                "\"messages\": %ld, \"tau\": [", n, halted, again, status, sent.load());
+                "\"control_loop_after_run\": %ld, \"run_after_request\": %ld, \"qp_status\": %d, "
+                "\"messages\": %ld, \"tau\": [", n, halted, again, pre, status, sent.load());
     for (int i = 0; i < numberOfJoints; ++i) std::printf("%s%.9g", i ? ", " : "", tau[i]);
     std::printf("]}\n");
     return status == WBC_QP_OK && wbc.qpReturnValue() == WBC_QP_OK ? 0 : 3;

@@ -219,8 +219,9 @@ long WholeBodyController::loop(long max_iterations, double rate_hz, const std::f
 }
 
 long WholeBodyController::run() {
-    // cpp:678-683: the control loop on its own thread, the callbacks on this one (ros::spin)
-    shutdown_.store(false);
+    // cpp:678-683: the control loop on its own thread, the callbacks on this one (ros::spin).
+    // shutdown_ is not cleared here either (as controlLoop): a requestShutdown() from another thread
+    // before run() is not dropped; resetShutdown() clears it for a new run
     std::atomic<bool> finished{false};
     std::exception_ptr err;
     long cycles = 0;

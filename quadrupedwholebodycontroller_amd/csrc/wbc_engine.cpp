@@ -8,8 +8,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 
 #include "wbc.h"
 #include "wbc_anymal_model.h"
@@ -242,24 +244,50 @@ hipError_t resident_alloc(wbc_engine* h) {
     return e;
 }
 
+// At most one resident wave runs per process: a resident kernel holds its hardware queue
+// between cycles, and streams share the GPU_MAX_HW_QUEUES queues, so another engine's work could wait
+// behind it until its idle exit.  g_res_owner is the engine whose wave runs; every start and stop of a
+// resident wave holds g_res_mu, and every other engine's call that launches work stops that wave first
+// (sync_own).  Streams of other libraries (torch) are not covered: INTEGRATION.md states the limit.
+std::recursive_mutex g_res_mu;
+wbc_engine* g_res_owner = nullptr;
+
 // The resident cycle's wave (WBC_RESIDENT) ends: WBC_RESIDENT_STOP posted, then its stream drained
-// (it may have ended by itself after its idle time: then the sync returns at once).
+// (it may have ended by itself after its idle time: then it is idle at once).  Bounded: a wave that
+// does not end within kResidentStopWait (stuck inside a step) is reported, not waited for forever.
+constexpr auto kResidentStopWait = std::chrono::seconds(2);
 hipError_t resident_stop(wbc_engine* h) {
+    std::lock_guard<std::recursive_mutex> lk(g_res_mu);
     if (!h->res_on) return hipSuccess;
     h->res_on = false;
+    if (g_res_owner == h) g_res_owner = nullptr;
     __atomic_store_n(&h->res_box->cmd, wbc::WBC_RESIDENT_STOP, __ATOMIC_RELEASE);
-    const hipError_t e = hipStreamSynchronize(h->res_stream);
+    const auto deadline = std::chrono::steady_clock::now() + kResidentStopWait;
+    hipError_t e;
+    while ((e = hipStreamQuery(h->res_stream)) == hipErrorNotReady) {
+        if (std::chrono::steady_clock::now() > deadline) return hipErrorLaunchTimeOut;
+        std::this_thread::yield();
+    }
     __atomic_store_n(&h->res_box->cmd, h->res_seq, __ATOMIC_RELEASE);  // the next wave starts from res_seq
     return e;
+}
+
+// Another engine's resident wave on this engine's device, stopped before this engine launches work.
+hipError_t stop_foreign_resident(wbc_engine* h) {
+    std::lock_guard<std::recursive_mutex> lk(g_res_mu);
+    if (!g_res_owner || g_res_owner == h || g_res_owner->device != h->device) return hipSuccess;
+    return resident_stop(g_res_owner);
 }
 
 // After a zero-copy wbc_cycle the cycle's inputs, outputs and wave map live in the pinned blocks;
 // copy them into the engine's own device buffers, so every other call sees the state a copying
 // cycle leaves (synchronous: the pinned blocks are rewritten by the next cycle).  A resident cycle
-// wave is stopped first (every other call goes through here).
+// wave is stopped first, this engine's or another engine's on the same device (every other call goes
+// through here).
 hipError_t sync_own(wbc_engine* h) {
-    if (h->res_on) {
-        const hipError_t e = resident_stop(h);
+    {
+        hipError_t e = resident_stop(h);
+        if (e == hipSuccess) e = stop_foreign_resident(h);
         if (e != hipSuccess) return e;
     }
     if (!h->zc_stale) return hipSuccess;
@@ -770,12 +798,18 @@ constexpr auto kResidentRestart = std::chrono::milliseconds(40);
 constexpr auto kResidentAnswer = std::chrono::seconds(2);
 int32_t resident_cycle(wbc_engine* h, uint32_t flags) {
     using clk = std::chrono::steady_clock;
+    std::lock_guard<std::recursive_mutex> lk(g_res_mu);
+    // wbc_cycle has written this cycle's pinned inputs and the host's mask count / map: the own
+    // buffers follow them at the next sync_own whether or not the cycle below succeeds (as
+    // enqueue_cycle does on every path), so d_contacts never lags n_stance_own / h_qmap
+    h->zc_stale = true;
     const size_t B = (size_t)h->batch;
+    WBC_HIP(stop_foreign_resident(h));
     if (h->res_on && (h->res_flags != flags || clk::now() - h->res_last > kResidentRestart)) WBC_HIP(resident_stop(h));
-    if (!h->res_on) {
-        if (!h->res_box) WBC_HIP(resident_alloc(h));
+    const auto launch = [&](unsigned long long seq0) -> hipError_t {
         // work queued on the engine stream (a reset, copies) completes before the wave reads the history
-        WBC_HIP(hipStreamSynchronize(h->stream));
+        hipError_t e = hipStreamSynchronize(h->stream);
+        if (e != hipSuccess) return e;
         // the step reads the engine's own device input block (the wave copies the pinned block into it
         // every cycle) and writes the pinned output block through its device address
         const double* ib = static_cast<const double*>(h->d_inblk);
@@ -795,25 +829,41 @@ int32_t resident_cycle(wbc_engine* h, uint32_t flags) {
         a.elim = 1;  // as begin_step16: the default step
         a.qmap = nullptr;  // one wave: its robots in batch order
         a.nwaves = 1;
-        __atomic_store_n(&h->res_box->cmd, h->res_seq, __ATOMIC_RELEASE);
+        __atomic_store_n(&h->res_box->exited, 0ull, __ATOMIC_RELEASE);
         const int words = (int)((in_block_bytes(B) + 7) / 8);
-        WBC_HIP(wbc_launch_resident(&a, h->res_box_dev, h->m_in, h->d_inblk, words, h->res_seq, kResidentIdleTicks,
-                                    h->res_stream));
+        e = wbc_launch_resident(&a, h->res_box_dev, h->m_in, h->d_inblk, words, seq0, kResidentIdleTicks, h->res_stream);
+        if (e != hipSuccess) return e;
         h->res_on = true;
         h->res_flags = flags;
+        g_res_owner = h;
+        return hipSuccess;
+    };
+    if (!h->res_on) {
+        if (!h->res_box) WBC_HIP(resident_alloc(h));
+        __atomic_store_n(&h->res_box->cmd, h->res_seq, __ATOMIC_RELEASE);
+        WBC_HIP(launch(h->res_seq));
     }
     const unsigned long long seq = ++h->res_seq;
     __atomic_store_n(&h->res_box->cmd, seq, __ATOMIC_RELEASE);  // the inputs (pinned) are written before
     const auto deadline = clk::now() + kResidentAnswer;
+    bool relaunched = false;
     while (__atomic_load_n(&h->res_box->done, __ATOMIC_ACQUIRE) != seq) {
+        if (!relaunched && __atomic_load_n(&h->res_box->exited, __ATOMIC_ACQUIRE) == 1ull &&
+            __atomic_load_n(&h->res_box->done, __ATOMIC_ACQUIRE) != seq) {
+            // the wave reached its idle limit just before this cycle was posted (the host thread
+            // stalled past kResidentRestart's margin): start a new one from the previous cycle; it
+            // picks the posted cycle up
+            h->res_on = false;
+            WBC_HIP(launch(seq - 1));
+            relaunched = true;
+        }
         if (clk::now() > deadline) {
-            (void)resident_stop(h);  // (the wave ends by itself within its idle limit)
+            (void)resident_stop(h);
             return fail(WBC_ERR_HIP, "wbc_cycle: the resident step did not answer");
         }
         __builtin_ia32_pause();
     }
     h->res_last = clk::now();
-    h->zc_stale = true;  // the own buffers lag the pinned blocks until sync_own, as after a zero-copy cycle
     return WBC_OK;
 }
 }  // namespace

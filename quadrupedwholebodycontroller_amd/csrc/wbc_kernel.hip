@@ -332,6 +332,17 @@ __device__ __forceinline__ int wave_select_band(double v, double& m) {
     return b ? __builtin_ctzll(b) : 0;
 }
 
+// max |v| over the wave (uniform): the DPP min chain of wave_select_band on -|v|
+__device__ __forceinline__ double wave_absmax(double v) {
+    double w = dpp_min<0x128, 0xF>(-fabs(v));  // row_ror:8
+    w = dpp_min<0x124, 0xF>(w);                 // row_ror:4
+    w = dpp_min<0x122, 0xF>(w);                 // row_ror:2
+    w = dpp_min<0x121, 0xF>(w);                 // row_ror:1
+    w = dpp_min<0x142, 0xA>(w);                 // row_bcast:15 into rows 1, 3
+    w = dpp_min<0x143, 0xC>(w);                 // row_bcast:31 into rows 2, 3
+    return -bcast(w, 63);
+}
+
 // Sum over the 16 lanes of each DPP row (row_ror 8, 4, 2, 1); lane 0's value is broadcast so the
 // result is uniform.  Used for the 13-body sums of the update phase (lanes >= 13 pass 0).
 __device__ __forceinline__ double row0_sum(double v) {
@@ -3892,8 +3903,11 @@ __device__ void solve_phase(const KernelArgs& a, int rb, const Prob& P, const Pr
             double t1;
             int l1;
             {
+                // an r_k at rounding level next to the largest |r| is no drop candidate (WBC_R_REL,
+                // include/wbc.h; the C oracle's literal form applies the same rule)
+                const double rthr = fmax(1e-14, WBC_R_REL * wave_absmax(lane < q ? rk : 0.0));
                 double v = 1e300;
-                if (lane < q && lane >= neq_added && rk > 1e-14) v = u * fast_rcp(rk);
+                if (lane < q && lane >= neq_added && rk > rthr) v = u * fast_rcp(rk);
                 l1 = wave_argmin_lane(v);
                 t1 = bcast(v, l1);
             }
@@ -4690,8 +4704,12 @@ WBC_UPDATE_KERNEL_ATTR void wbc_resident_kernel(KernelArgs args, ResidentBox* bo
             for (;;) {
                 c = __hip_atomic_load(&bx->cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (c != last) break;
-                if (__builtin_amdgcn_s_memrealtime() - t0 > idle) { c = WBC_RESIDENT_STOP; break; }
-                __builtin_amdgcn_s_sleep(1);
+                const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
+                if (dt > idle) { c = WBC_RESIDENT_STOP; break; }
+                // polls over PCIe: every ~30 ns for the first 100 us after a cycle (a control loop's
+                // next cycle usually comes sooner), then every ~0.5 us
+                if (dt < 10000ull) __builtin_amdgcn_s_sleep(1);
+                else __builtin_amdgcn_s_sleep(16);
             }
             C.cmd = c;
         }
@@ -4755,6 +4773,7 @@ WBC_UPDATE_KERNEL_ATTR void wbc_resident_kernel(KernelArgs args, ResidentBox* bo
             C.last = cmd;
         }
     }
+    if (threadIdx.x == 0) __hip_atomic_store(&C.box->exited, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 #ifdef WBC_MODES_TU  // (wbc_kernel_modes.hip)

@@ -119,13 +119,16 @@ inline void build_lds_image(const wbc_model& m, double friction, LdsImage& o) {
 
 // The resident control cycle's mailbox (wbc_cycle with WBC_RESIDENT; pinned, coherent host memory):
 // the host raises cmd (a sequence number, or WBC_RESIDENT_STOP), the resident wave answers with
-// done = cmd once the cycle's outputs are visible.  The two words sit on separate 64-byte lines.
+// done = cmd once the cycle's outputs are visible, and sets exited = 1 when it ends (on
+// WBC_RESIDENT_STOP or after its idle limit), so the host can tell a wave that ended by itself from
+// one that is late.  cmd and the wave's words sit on separate 64-byte lines.
 constexpr unsigned long long WBC_RESIDENT_STOP = ~0ull;
 struct ResidentBox {
     unsigned long long cmd;
     unsigned long long pad0[7];
     unsigned long long done;
-    unsigned long long pad1[7];
+    unsigned long long exited;
+    unsigned long long pad1[6];
 };
 
 // Kernel arguments (one struct, passed by value).

@@ -72,6 +72,8 @@ def test_controller_run_spins_callbacks_beside_the_control_thread():
     # controlLoop() runs nothing until resetShutdown(), then its own cycles
     assert res["control_loop_after_shutdown"] == 0
     assert res["control_loop_after_run"] == 25
+    # a requestShutdown() issued before run() is not cleared by run(): no cycle runs
+    assert res["run_after_request"] == 0
     s = subprocess.run([BIN, "stance", "300"], capture_output=True, text=True, timeout=300)
     ref = json.loads(s.stdout.strip().splitlines()[-1])
     assert close_to(res["tau"], ref["tau"], M.REPLAY, "tau"), (res["tau"], ref["tau"])

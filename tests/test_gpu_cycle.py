@@ -198,3 +198,44 @@ def test_resident_cycle_stateless_and_above_limit(B):
             assert np.array_equal(got[k], want[k]), (t, k)
     e1.close()
     e2.close()
+
+
+def test_two_resident_engines_in_turn():
+    """Two B = 1 engines cycled in turn with WBC_RESIDENT: at most one resident wave
+    runs per process, and any other engine's call stops it first, so neither engine's work can
+    queue behind the other's polling wave on a shared hardware queue (it would wait up to the
+    wave's 100 ms idle limit).  Both trajectories equal separate plain steps bit for bit, no cycle
+    takes more than 20 ms and the median stays under 2 ms; a large engine's step issued while a
+    resident wave runs is not held up either."""
+    import time
+
+    seqs = [list(workloads.trot_sequence(1, steps=60, seed=s)) for s in (13, 14)]
+    plain = [Engine(1), Engine(1)]
+    res = [Engine(1), Engine(1)]
+    big = Engine(4096)
+    binp = workloads.stance_cold(4096, seed=3)
+    big.set_state(binp["base_pose"], binp["nu"], binp["qj"])
+    big.set_reference(binp["ref"], binp["contacts"], binp["switching"])
+    big.step(STATELESS)
+    want_big = big.outputs()
+    dts, big_dts = [], []
+    for t in range(60):
+        for i in (0, 1):
+            s = seqs[i][t]
+            want = separate_calls(plain[i], s, 0)
+            t0 = time.perf_counter()
+            got = res[i].cycle(s["base_pose"], s["nu"], s["qj"], s["ref"], s["contacts"], s["switching"], RESIDENT)
+            dts.append(time.perf_counter() - t0)
+            for k in KEYS:
+                assert np.array_equal(got[k], want[k]), (t, i, k)
+        if t % 10 == 5:  # a large engine's step while engine 1's resident wave runs
+            t0 = time.perf_counter()
+            big.step(STATELESS)
+            o = big.outputs()
+            big_dts.append(time.perf_counter() - t0)
+            assert np.array_equal(o["tau"], want_big["tau"])
+    for e in plain + res + [big]:
+        e.close()
+    dts = np.array(dts[2:])  # (the first cycles start the waves)
+    assert dts.max() < 0.02 and np.median(dts) < 0.002, (dts.max(), np.median(dts))
+    assert max(big_dts) < 0.02, big_dts
