@@ -543,6 +543,7 @@ def main():
                              "solves); latency/issue-bound small dense linear algebra",
                      "flops_per_launch": flops_step,
                      "traffic_calibration": (pmc_rec or {}).get("calibration"),
+                     "traffic_split": (pmc_rec or {}).get("traffic_split"),
                      "executed_fp64": executed_fp64(args.config, B, dom, dom_ms)},
         "roofline_hbm": {"bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": hbm_gbs / HBM_PEAK_GBS, "bytes_per_solve": bytes_step / B,

@@ -102,6 +102,21 @@ __global__ __launch_bounds__(64) void calib_rows_modes(Rows r, int S, int K, int
         if (wr) write_out(r, row * K + c * M + h, lane, v + h);
 }
 
+// A long straight-line body with no data reads: 24576 dependent v_fma_f64 on
+// registers, ~96 KB of code, 1024 workgroups.  Its FETCH_SIZE is the instruction fetch a launch makes
+// from HBM (each XCD's L2 misses the code once); the known bytes are 8 x its symbol size
+// (tools/calib_summary.py reads the size from this binary's code object).
+#define CODE_F1 a = fma(a, b, a);
+#define CODE_F8 CODE_F1 CODE_F1 CODE_F1 CODE_F1 CODE_F1 CODE_F1 CODE_F1 CODE_F1
+#define CODE_F64 CODE_F8 CODE_F8 CODE_F8 CODE_F8 CODE_F8 CODE_F8 CODE_F8 CODE_F8
+#define CODE_F512 CODE_F64 CODE_F64 CODE_F64 CODE_F64 CODE_F64 CODE_F64 CODE_F64 CODE_F64
+#define CODE_F4096 CODE_F512 CODE_F512 CODE_F512 CODE_F512 CODE_F512 CODE_F512 CODE_F512 CODE_F512
+__global__ __launch_bounds__(64) void calib_code(double seed, double* out) {
+    double a = seed + (double)threadIdx.x, b = seed * 0.5;
+    CODE_F4096 CODE_F4096 CODE_F4096 CODE_F4096 CODE_F4096 CODE_F4096  // straight-line: a loop would be a few hundred bytes of code
+    if (a == 12345.0) out[blockIdx.x] = a;  // never true: no write bytes
+}
+
 __global__ __launch_bounds__(64) void calib_image(const double* limg, double* out) {
     double acc = 0.0;
     for (int k = threadIdx.x; k < wbc::LIMG_LEN; k += 64) acc += limg[k];
@@ -188,6 +203,7 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL(calib_rows_rl, dim3(waves2), dim3(64), 0, 0, r2, dmap);
         hipLaunchKernelGGL(calib_rows_modes, dim3(waves3), dim3(64), 0, 0, r3, S, K, M);
         hipLaunchKernelGGL(calib_image, dim3(1024), dim3(64), 0, 0, limg, sink);
+        hipLaunchKernelGGL(calib_code, dim3(1024), dim3(64), 0, 0, 1e-9, sink);
         hipLaunchKernelGGL(calib_stream16, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, 0, src, sink, n2);
     }
     CK(hipDeviceSynchronize());
@@ -199,6 +215,7 @@ int main(int argc, char** argv) {
                 "\"calib_rows_rl\": {\"read\": %.0f, \"write\": %.0f, \"qps\": %d, \"waves\": %d}, "
                 "\"calib_rows_modes\": {\"read\": %.0f, \"write\": %.0f, \"qps\": %d, \"waves\": %d}, "
                 "\"calib_image\": {\"read_per_workgroup\": %.0f, \"workgroups\": 1024, \"write\": 0}, "
+                "\"calib_code\": {\"workgroups\": 1024, \"write\": 0, \"code\": \"8 x the symbol size\"}, "
                 "\"calib_stream16\": {\"read\": %.0f, \"write\": 0}}\n",
                 launches, B1 * in_row, B1 * out_qp, B1, B2 * in_row_nocon + waves2 * 16.0, B2 * out_qp, B2, waves2,
                 S * in_row_nocon, (double)S * K * out_qp, S * K, waves3, wbc::LIMG_LEN * 8.0, n2 * 16.0);

@@ -83,6 +83,37 @@ def calibration(workload):
     return None
 
 
+# the step kernel instance each bench workload launches (its code is what the L2s fetch)
+STEP_INSTANCE = {"stance_cold": r"wbc_update_solve_kernelILi0ELb1E", "rl_random": r"wbc_update_solve_kernelILi0ELb0E",
+                 "trot": r"wbc_update_solve_kernelILi1ELb0E", "modes16": r"wbc_modes_kernel"}
+
+
+def code_calibration():
+    """(code_factor, source): how FETCH_SIZE counts instruction fetch, from the newest calibration
+    record with a calib_code entry (tools/micro/calib.hip), or None."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for f in sorted(glob.glob(os.path.join(root, "profiles", "*", "calib", "calib_summary.json")), reverse=True):
+        k = json.load(open(f))["kernels"].get("calib_code", {})
+        if "code_factor" in k:
+            return k["code_factor"], os.path.relpath(f, root) + ":calib_code"
+    return None
+
+
+def step_code_bytes(workload, lib=None):
+    """HBM bytes of instruction fetch per launch of the workload's step kernel: 8 XCD L2s x its code
+    size in the engine library (tools/code_size.py), or None."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from code_size import XCDS, code_size
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = lib or os.path.join(root, "quadrupedwholebodycontroller_amd", "libwbc_hip.so")
+    pat = next((v for k, v in STEP_INSTANCE.items() if workload.startswith(k)), None)
+    if not pat or not os.path.exists(lib):
+        return None
+    cs = code_size(lib, pat)
+    return XCDS * cs if cs else None
+
+
 def main():
     pmc_dir, out = sys.argv[1], sys.argv[2]
     workload = sys.argv[3] if len(sys.argv) > 3 else "stance_cold_b4096"
@@ -111,6 +142,19 @@ def main():
     # the step's kernels that ran (the default step runs one of them: wbc_update_solve_kernel, or
     # wbc_modes_kernel for mode hypotheses under the mode loop)
     ran = [k for k in step_kernels if traffic.get(k) is not None]
+    # instruction fetch: FETCH_SIZE also counts the step kernel's code, fetched from
+    # HBM once per XCD and counted with its own factor (calib_code), not the data pattern's; split it
+    # off so the data bytes are scaled by the data factor only, and add the code bytes back as is
+    cc, code = code_calibration(), step_code_bytes(workload)
+    if cal and cc and code and len(ran) == 1 and "FETCH_SIZE" in mean[ran[0]]:
+        m = mean[ran[0]]
+        code_counted = code / cc[0]
+        data = rf * (m["FETCH_SIZE"] * 1024.0 - code_counted) + wf * m["WRITE_SIZE"] * 1024.0
+        traffic[ran[0]] = data + code
+        rec["traffic_split"] = {"data": data, "code_fetch": code, "code_factor": cc[0], "code_source": cc[1],
+                                "note": "code_fetch = 8 XCD L2s x the step kernel's code size (tools/code_size.py); "
+                                        "data = (FETCH_SIZE - code_fetch / code_factor) x read_factor + "
+                                        "WRITE_SIZE x write_factor"}
     if ran:
         traffic["step"] = sum(traffic[k] for k in ran)
     rec["traffic"] = traffic
