@@ -75,13 +75,17 @@ def test_full_batch_sample_matches_oracle_and_small_batch(name, B, seed):
         assert np.array_equal(small[k], out[k][rows]), k
 
 
-def test_modes_full_shard_sample_matches_oracle_and_small_batch():
-    S, K = 1024, 16
+@pytest.mark.parametrize("S", [1024, 8192])
+def test_modes_full_shard_sample_matches_oracle_and_small_batch(S):
+    """S = 1024: the configs[4] shard of one GPU of eight; S = 8192: configs[4]'s global batch
+    (131 072 QPs) on one GPU."""
+    K = 16
     inp, modes = workloads.mode_states(S, 4)
     out = run(inp, modes)
     # 40 spread states plus the pass boundaries (QP 2048 k = state 128 k) and the last state
-    states = np.unique(np.concatenate([np.linspace(0, S - 1, 40).astype(int), np.arange(127, S, 128),
-                                       np.arange(128, S, 128), [S - 1]]))
+    step = 128 if S <= 1024 else 1024
+    states = np.unique(np.concatenate([np.linspace(0, S - 1, 40).astype(int), np.arange(step - 1, S, step),
+                                       np.arange(step, S, step), [S - 1]]))
     rows = (states[:, None] * K + np.arange(K)[None, :]).ravel()
     assert len(rows) >= 512 and rows[-1] == S * K - 1
     # the oracle sees each hypothesis as its own robot (contacts = modes[k])

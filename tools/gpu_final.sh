@@ -5,7 +5,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 TAG=${TAG:-final}
-ROUND=${ROUND:-r05}
+ROUND=${ROUND:-r06}
 O=gpurun_out/$TAG
 mkdir -p $O profiles/$ROUND
 step() { local name=$1 t=$2; shift 2; echo "== $name $(date +%T)"; timeout -k 10 $t "$@" > $O/$name.log 2>&1; local rc=$?; echo "== $name rc=$rc"; if [ $rc -ne 0 ]; then tail -30 $O/$name.log; exit $rc; fi; }
@@ -26,9 +26,9 @@ fi
 if [ $PART = 1 ]; then echo part1 done; exit 0; fi
 step bench 300 python bench.py --steps 50 --warmup 5
 step bench_extra 300 python bench.py --steps 20 --warmup 3 --extra --breakdown --no-cpu-baseline
-step prof 300 rocprofv3 --kernel-trace --stats -d $O/prof -o prof --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline
+step prof 300 rocprofv3 --kernel-trace --stats -d $O/prof -o prof --output-format csv -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline
 for cb in rl_random_b8192 modes16_b16384; do
-  step prof_$cb 300 rocprofv3 --kernel-trace --stats -d $O/prof_$cb -o prof --output-format csv -- python3 bench.py --config $cb --steps 50 --warmup 5 --no-cpu-baseline
+  step prof_$cb 300 rocprofv3 --kernel-trace --stats -d $O/prof_$cb -o prof --output-format csv -- python3 bench.py --config $cb --steps 200 --warmup 20 --no-cpu-baseline
 done
 step b1_fused 120 quadrupedwholebodycontroller_amd/wbc_control_loop stance 3000 0 fused
 step b1_launch 120 quadrupedwholebodycontroller_amd/wbc_control_loop stance 3000 0 launch
