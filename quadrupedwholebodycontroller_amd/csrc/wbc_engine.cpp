@@ -520,7 +520,11 @@ int32_t wbc_destroy(wbc_engine* h) {
     // drain the engine's in-flight work before freeing (the bound stream; never the whole device,
     // which would also wait for other engines' and the caller's unrelated work)
     (void)drain(h);
-    (void)resident_stop(h);
+    {
+        std::lock_guard<std::recursive_mutex> lk(g_res_mu);
+        (void)resident_stop(h);
+        if (g_res_owner == h) g_res_owner = nullptr;  // never left pointing at a freed engine
+    }
     if (h->res_box) (void)hipHostFree(h->res_box);
     if (h->res_stream) (void)hipStreamDestroy(h->res_stream);
     void* ptrs[] = {h->d_model, h->d_params, h->d_limg, h->d_inblk, h->d_outblk, h->d_mask, h->d_modes, h->d_hist, h->d_work,
@@ -854,6 +858,7 @@ int32_t resident_cycle(wbc_engine* h, uint32_t flags) {
             // stalled past kResidentRestart's margin): start a new one from the previous cycle; it
             // picks the posted cycle up
             h->res_on = false;
+            if (g_res_owner == h) g_res_owner = nullptr;  // (launch sets it again on success)
             WBC_HIP(launch(seq - 1));
             relaunched = true;
         }

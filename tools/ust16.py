@@ -2,26 +2,28 @@
 reduced to 12 variables and solved in its 16-lane segment), from the WBC_ISTAMPS build: medians over
 waves (lane 0 of each wave writes the stamps, so only QPs qp % 4 == 0 carry them).
 Usage (GPU box): WBC_LIB=quadrupedwholebodycontroller_amd/libwbc_hip_istamps.so python tools/ust16.py [config] [B]
-(config: a stateless workloads generator, or trot: configs[2]'s stateful trot, its 60th cycle)"""
+(config: a stateless workloads generator, or trot: configs[2]'s stateful trot, its 60th cycle;
+WBC_UST_NOX=1 steps with WBC_NO_X, as bench.py does)"""
 import json, os, sys
 import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from quadrupedwholebodycontroller_amd import STATELESS, Engine, workloads
+from quadrupedwholebodycontroller_amd import NO_X, STATELESS, Engine, workloads
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "stance_cold"
+XF = NO_X if os.environ.get("WBC_UST_NOX") else 0
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
 e = Engine(B)
 if cfg == "trot":  # configs[2]: stateful (history, hotstart), the stamps of its 60th cycle
     for k, s in enumerate(workloads.trot_sequence(B, steps=60, seed=2)):
         e.set_state(s["base_pose"], s["nu"], s["qj"])
         e.set_reference(s["ref"], s["contacts"], s["switching"])
-        e.step(0)
+        e.step(XF)
 else:
     inp = getattr(workloads, cfg)(B, seed=1 if cfg == "stance_cold" else 3)
     e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
     e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
     for _ in range(3):
-        e.step(STATELESS)
+        e.step(STATELESS | XF)
 e.synchronize()
 D = e.debug()[0::4]
 st = lambda i: D[:, 8 + i]  # UST(i)
