@@ -152,15 +152,18 @@ dist.destroy_process_group()
 """
 
 
-def test_two_rank_gloo_shard_and_gather(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_two_rank_gloo_shard_and_gather(tmp_path, world):
+    """world_size 2 (the required rehearsal) and 4 (uneven shards of the odd batches, closer to the
+    8-GPU node): shard, gather, unpack, bit-identical to one full-batch run."""
     script = tmp_path / "worker.py"
     script.write_text(DIST_WORKER.format(root=ROOT))
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", "--master-port=29531", str(script)]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr=127.0.0.1", f"--master-port={29531 + world}", str(script)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
-    assert "DIST_OK 0" in r.stdout and "DIST_OK 1" in r.stdout
+    assert all(f"DIST_OK {k}" in r.stdout for k in range(world))
 
 
 def test_bench_world_mismatch_exits_nonzero():
