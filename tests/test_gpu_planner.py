@@ -8,7 +8,9 @@ message within 1e-12 (absolute + relative; the same fp64 expressions, up to FMA 
 import numpy as np
 import pytest
 
+import margins as M
 import planner_ref as PR
+import wbc_ref
 from quadrupedwholebodycontroller_amd import Engine, Planner, workloads
 
 pytestmark = pytest.mark.gpu
@@ -74,7 +76,9 @@ def test_planner_matches_reference_loop():
 
 def test_planner_drives_engine_on_device():
     """Planner tick every 4 control cycles (100 Hz vs 400 Hz); the engine reads the planner's
-    device buffers (no host copies) and matches the same run fed from host copies."""
+    device buffers (no host copies) and matches the same run fed from host copies bit for bit, and
+    the C oracle's stateful robots fed the same messages (status and iteration counts equal, tau at
+    the parity tolerance) through the planner's contact switches and the hotstart across them."""
     import torch
 
     B, cycles = 64, 4 * 85  # one full 4-step planner cycle
@@ -88,6 +92,7 @@ def test_planner_drives_engine_on_device():
     for e in (e_dev, e_host):
         e.set_state(st["base_pose"], st["nu"], st["qj"])
     e_dev.bind_device_inputs(ref=dev["ref"], contacts=dev["contacts"], switching=dev["switching"])
+    robots = wbc_ref.Robots(np.arange(B), method=wbc_ref.REDUCED)
     seen = set()
     for c in range(cycles):
         if c % 4 == 0:
@@ -99,6 +104,10 @@ def test_planner_drives_engine_on_device():
         a, h = e_dev.outputs(), e_host.outputs()
         for k in ("tau", "grf", "status"):
             assert np.array_equal(a[k], h[k]), (c, k)
+        r = robots.step(dict(st, ref=o["ref"], contacts=o["contacts"], switching=o["switching"]))
+        assert np.array_equal(a["status"], r["status"]) and np.array_equal(a["iters"], r["iters"]), c
+        ok = r["status"] == 0
+        assert M.close(a["tau"][ok], r["tau"][ok], M.TAU, "tau"), c
         seen.update(int(x) for x in o["contacts"])
     assert {7, 11, 13, 14} <= seen  # every single-swing mode was exercised
     for e in (e_dev, e_host):

@@ -250,3 +250,28 @@ def test_stateful_trot_with_stretched_legs_vs_c_oracle():
                 n_checked += 1
     e.close()
     assert n_checked > B * steps // 2
+
+
+def test_long_trot_no_drift_vs_c_oracle():
+    """2000 stateful cycles (5 s at 400 Hz, 20 contact switches) of 64 robots against the C
+    oracle's stateful robots (the REDUCED method: the same 12-variable form and hotstart): status and
+    iteration counts equal at every cycle, tau at the parity tolerance at every cycle.  The integral
+    error e_int and the finite-difference history accumulate over the whole run, so a bias in either
+    would grow here."""
+    B, steps = 64, 2000
+    robots = R.Robots(np.arange(B), method=R.REDUCED)
+    e = Engine(B)
+    worst = 0.0
+    for t, inp in enumerate(workloads.trot_sequence(B, steps=steps, seed=24)):
+        e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
+        e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
+        e.step(0)
+        o = e.outputs()
+        r = robots.step(inp)
+        assert np.array_equal(o["status"], r["status"]) and np.array_equal(o["iters"], r["iters"]), t
+        ok = r["status"] == 0
+        assert close_to(o["tau"][ok], r["tau"][ok], M.TAU, "tau"), t
+        worst = max(worst, M.norm_err(o["tau"][ok], r["tau"][ok]))
+    e.close()
+    # the error at the end of the run is no larger than the bound either (no growth with time)
+    assert worst <= M.TAU
