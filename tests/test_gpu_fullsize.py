@@ -153,3 +153,29 @@ def test_trot_bench_path_every_step_matches_stateful_oracle():
         if p == 0:
             assert n_ok > 0.9 * len(rows) * T
     e.close()
+
+
+@pytest.mark.parametrize("name,B,seed", [("rl_random", 8192, 3), ("stance_cold", 4096, 1)])
+def test_split_form_full_batch_matches_literal_oracle(name, B, seed):
+    """The reference's updateState() / solveQP() surface at the bench's sizes: WBC_SPLIT (the update
+    kernel, the problem through HBM, then the 24-variable solve kernel, one robot per wave, several
+    occupancy passes) against the oracle's LITERAL method on the 42 x 70 QP: identical status and
+    iteration counts on a stratified sample of >= 512 rows, tau at the parity tolerance."""
+    from quadrupedwholebodycontroller_amd import SPLIT
+
+    inp = getattr(workloads, name)(B, seed=seed)
+    e = Engine(B)
+    e.set_state(inp["base_pose"], inp["nu"], inp["qj"])
+    e.set_reference(inp["ref"], inp["contacts"], inp["switching"])
+    e.step(STATELESS | SPLIT)
+    out = e.outputs()
+    e.close()
+    rows = sample_rows(B)
+    sub = {k: np.ascontiguousarray(v[rows]) for k, v in inp.items()}
+    o = R.run_batch(sub, method=R.LITERAL)
+    assert np.array_equal(out["status"][rows], o["status"])
+    same = out["iters"][rows] == o["iters"]
+    assert M.record("iters mismatch fraction (split)", 1.0 - same.mean(), 0.0) == 0.0, rows[~same][:8]
+    ok = o["status"] == 0
+    assert M.close(out["tau"][rows][ok], o["tau"][ok], M.TAU, "tau")
+    assert M.close(out["x"][rows][ok], o["x"][ok], M.X, "x")
