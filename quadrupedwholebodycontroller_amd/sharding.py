@@ -137,17 +137,20 @@ def all_gather_rows(local, world: int, group=None):
 class StepPipeline:
     """The per-step loop of bench.py on N ranks: every step writes the rank's outputs straight into a
     packed block (StepOutputs, bound as the engine's output buffers) and the step's one collective
-    gathers the blocks on a second stream, overlapped with the next step.  Two blocks alternate: step
-    k + 2 waits for the gather of step k (an event on `comm`) before the engine overwrites its block.
+    gathers the blocks on a second stream, overlapped with the next steps.  `nbuf` blocks rotate: step
+    k + nbuf waits for the gather of step k (an event on `comm`) before the engine overwrites its block.
 
     engine: the rank's Engine (on `stream`); step(flags) runs one step (Engine.step or step_modes);
     cap: rows of a block (the largest shard).  With world == 1 there is no gather (the block is the
     whole batch's output).  tests/test_gpu_pipeline.py runs this class with two gloo ranks on one GPU
     and checks every step's gathered outputs against a one-rank step."""
 
-    def __init__(self, engine, step, flags, world, cap, stream, comm=None, device="cuda", group=None, collective=None):
+    def __init__(self, engine, step, flags, world, cap, stream, comm=None, device="cuda", group=None, collective=None,
+                 nbuf=3):
         """collective: gather every step (default: world > 1); True with world == 1 runs the gather
-        path on a one-rank process group (tests/test_gpu_rccl.py)."""
+        path on a one-rank process group (tests/test_gpu_rccl.py).  nbuf: output blocks in rotation,
+        so that a gather may take up to nbuf - 1 steps before the compute stream waits for it (three:
+        one RCCL all-gather of an 8-rank step is about as long as the step itself)."""
         import torch
 
         self.torch = torch
@@ -155,12 +158,13 @@ class StepPipeline:
         self.coll = (world > 1) if collective is None else bool(collective)
         self.stream, self.comm, self.group = stream, comm, group
         self.cap = cap
-        self.blocks = [StepOutputs(cap, device=device) for _ in range(2)]
+        self.nbuf = max(2, int(nbuf))
+        self.blocks = [StepOutputs(cap, device=device) for _ in range(self.nbuf)]
         self.gathered = ([torch.empty(world * cap * ROW_DOUBLES, dtype=torch.float64, device=device)
-                          for _ in range(2)] if self.coll else None)
-        self.ev_step = [torch.cuda.Event() for _ in range(2)]
-        self.ev_gath = [torch.cuda.Event() for _ in range(2)]
-        self.used = [False, False]
+                          for _ in range(self.nbuf)] if self.coll else None)
+        self.ev_step = [torch.cuda.Event() for _ in range(self.nbuf)]
+        self.ev_gath = [torch.cuda.Event() for _ in range(self.nbuf)]
+        self.used = [False] * self.nbuf
         self.k = 0
 
     def bind(self, slot):
@@ -170,9 +174,9 @@ class StepPipeline:
     def step(self):
         """Queue one step (and, N > 1, its gather); returns the slot its outputs land in."""
         torch = self.torch
-        slot = self.k & 1
+        slot = self.k % self.nbuf
         if self.coll and self.used[slot]:
-            self.stream.wait_event(self.ev_gath[slot])  # the gather of step k - 2 has read this block
+            self.stream.wait_event(self.ev_gath[slot])  # the gather of step k - nbuf has read this block
         self.bind(slot)
         self.step_fn(self.flags)
         if self.coll:
@@ -188,7 +192,11 @@ class StepPipeline:
 
     @property
     def last_slot(self):
-        return (self.k - 1) & 1
+        return (self.k - 1) % self.nbuf
+
+    def prev_slot(self, slot):
+        """The slot of the step queued before the one in `slot`."""
+        return (slot - 1) % self.nbuf
 
     def result(self, slot, total, unit=1):
         """(tau, status, iters) of the step in `slot` for the whole batch (numpy, global order) once its

@@ -4,7 +4,7 @@ ranks sharing cuda:0 before the driver's first 8-GPU run executes it over RCCL.
 Each rank owns a contiguous shard of a global batch (strong scaling, as bench.py's rl_random_b65536 /
 modes16_x8192 configs; mode hypotheses shard by state), stages the inputs of every step in HBM and
 binds them per step (no host copy between steps, so the gather of step k, queued on the second
-stream, really overlaps step k + 1, and step k + 2 waits for it before reusing the block).  For each
+stream, really overlaps step k + 1, and step k + 3 waits for it before reusing the block).  For each
 of 8 steps with changing inputs, the gathered tau | status | iters of the whole batch must equal a
 one-rank step of the full batch on the same inputs, bit for bit: the step groups QPs by contact mask,
 so a robot's result does not depend on where the shard boundary falls."""
@@ -59,7 +59,7 @@ def run(name, inp_all, modes):
         e.bind_device_inputs(*[dev[kk][k].data_ptr() for kk in KEYS])
         slot = pipe.step()
         if k >= 1:  # the previous step's gather, read while this step runs
-            results.append(pipe.result(1 - slot, total, unit=K or 1))
+            results.append(pipe.result(pipe.prev_slot(slot), total, unit=K or 1))
     results.append(pipe.result(pipe.last_slot, total, unit=K or 1))
     torch.cuda.synchronize()
     e.close()

@@ -79,7 +79,7 @@ for k in range(STEPS):
     e.bind_device_inputs(*[dev[kk][k].data_ptr() for kk in KEYS])
     slot = pipe.step()
     if k >= 1:  # the previous step's gather, read while this step runs
-        results.append(pipe.result(1 - slot, B))
+        results.append(pipe.result(pipe.prev_slot(slot), B))
 results.append(pipe.result(pipe.last_slot, B))
 torch.cuda.synchronize()
 dist.barrier()
